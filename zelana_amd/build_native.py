@@ -1,0 +1,74 @@
+"""Build libzkmi.so in-tree (zelana_amd/libzkmi.so) for gfx950.
+
+hipcc cross-compiles the HIP translation units for gfx950 (no GPU needed);
+the host-only epilogue (msm_host.cpp) is compiled by g++.  Objects are cached
+under zelana_amd/build/ and rebuilt when a source or header is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "build")
+LIB = os.path.join(HERE, "libzkmi.so")
+ARCH = os.environ.get("ZKMI_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+             "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(HERE, "..", "include", "zkmi.h")]
+
+
+def _stale(obj, src):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(f) > t for f in [src] + _headers())
+
+
+def _compile(src):
+    base = os.path.splitext(os.path.basename(src))[0]
+    obj = os.path.join(BUILD, base + ".o")
+    if not _stale(obj, src):
+        return obj, None
+    if src.endswith(".hip"):
+        cmd = [HIPCC] + HIP_FLAGS + ["-c", src, "-o", obj]
+    else:
+        cmd = ["g++"] + CXX_FLAGS + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, "FAILED: " + " ".join(cmd) + "\n" + r.stdout + r.stderr
+    return obj, None
+
+
+def build(verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+    jobs = min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        results = list(ex.map(_compile, srcs))
+    errs = [e for _, e in results if e]
+    if errs:
+        raise RuntimeError("\n".join(errs))
+    objs = [o for o, _ in results]
+    if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed: " + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)

@@ -1,0 +1,347 @@
+// ff.h — BN254 Fq / Fr arithmetic for CDNA4 (gfx950), host+device.
+//
+// Representation (MI355X-first, not arkworks' 4x64):
+//   * 9 limbs x 29 bits held in 32-bit VGPRs, Montgomery radix R = 2^261.
+//   * Product-scanning Montgomery multiplication: every partial product is one
+//     v_mad_u64_u32 into a single 64-bit column accumulator.  29-bit limbs leave
+//     headroom for 18 products per column (< 2^64) so no carry chains are needed
+//     inside a column (measured: v_mad_u64_u32 issues at the same rate as a
+//     plain VALU op on gfx950, see tools/mb_modmul.hip / profiles/).
+//   * Lazy reduction: mul accepts inputs < 8p with limbs < 1.5*2^30 and returns
+//     a value < 2p with normalised limbs (R > 32p), so no final subtraction.
+//     add/sub return normalised values in [0, 2p).
+//   * Storage in HBM/LDS-less paths is the packed 8 x u32 (256-bit) form.
+// The GPU's Montgomery radix differs from arkworks' (2^256); conversion happens
+// only at the boundary (canonical <-> internal), never in the hot loops.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define ZK_HD __host__ __device__ __forceinline__
+#else
+#define ZK_HD inline
+#endif
+
+namespace zk {
+
+constexpr int NL = 9;
+constexpr uint32_t LMASK = (1u << 29) - 1;
+
+struct Fe {
+  uint32_t v[NL];
+};
+
+// Base field q (G1/G2 coordinates)
+struct FqP {
+  static constexpr uint32_t P[NL] = {0x187cfd47u, 0x010460b6u, 0x1c72a34fu, 0x02d522d0u, 0x1585d978u,
+                                     0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
+  static constexpr uint32_t P2[NL] = {0x10f9fa8eu, 0x0208c16du, 0x18e5469eu, 0x05aa45a1u, 0x0b0bb2f0u,
+                                      0x05b68181u, 0x014dc282u, 0x1cb84c68u, 0x0060c89cu};
+  static constexpr uint32_t PINV = 0x04866389u;  // -p^-1 mod 2^29
+  static constexpr uint32_t ONE[NL] = {0x157ccc21u, 0x141c2758u, 0x185230d3u, 0x014c0419u, 0x0aa36fb9u,
+                                       0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};  // R mod p
+  static constexpr uint32_t R2[NL] = {0x059bac10u, 0x0d1503a3u, 0x018016b8u, 0x10ab0ca8u, 0x02632639u,
+                                      0x02c0169fu, 0x169bfd53u, 0x11869d4cu, 0x002a11a6u};  // R^2 mod p
+};
+// Scalar field r (NTT domain)
+struct FrP {
+  static constexpr uint32_t P[NL] = {0x10000001u, 0x1f0fac9fu, 0x0e5c2450u, 0x07d090f3u, 0x1585d283u,
+                                     0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
+  static constexpr uint32_t P2[NL] = {0x00000002u, 0x1e1f593fu, 0x1cb848a1u, 0x0fa121e6u, 0x0b0ba506u,
+                                      0x05b68181u, 0x014dc282u, 0x1cb84c68u, 0x0060c89cu};
+  static constexpr uint32_t PINV = 0x0fffffffu;
+  static constexpr uint32_t ONE[NL] = {0x0fffff57u, 0x1ea70ab4u, 0x052c068bu, 0x17504f49u, 0x0aa8075bu,
+                                       0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};
+  static constexpr uint32_t R2[NL] = {0x05b69bd4u, 0x06170a5au, 0x020cddceu, 0x1db6310bu, 0x0e54d0ffu,
+                                      0x1cf855e3u, 0x1c15e103u, 0x07d09161u, 0x000a054au};
+};
+
+// ---------------------------------------------------------------- packing
+// 256-bit little-endian (8 x u32) <-> 9 x 29-bit limbs.
+ZK_HD Fe unpack(const uint32_t w[8]) {
+  Fe r;
+  r.v[0] = w[0] & LMASK;
+  r.v[1] = ((w[0] >> 29) | (w[1] << 3)) & LMASK;
+  r.v[2] = ((w[1] >> 26) | (w[2] << 6)) & LMASK;
+  r.v[3] = ((w[2] >> 23) | (w[3] << 9)) & LMASK;
+  r.v[4] = ((w[3] >> 20) | (w[4] << 12)) & LMASK;
+  r.v[5] = ((w[4] >> 17) | (w[5] << 15)) & LMASK;
+  r.v[6] = ((w[5] >> 14) | (w[6] << 18)) & LMASK;
+  r.v[7] = ((w[6] >> 11) | (w[7] << 21)) & LMASK;
+  r.v[8] = w[7] >> 8;
+  return r;
+}
+ZK_HD void pack(uint32_t w[8], const Fe& a) {
+  w[0] = a.v[0] | (a.v[1] << 29);
+  w[1] = (a.v[1] >> 3) | (a.v[2] << 26);
+  w[2] = (a.v[2] >> 6) | (a.v[3] << 23);
+  w[3] = (a.v[3] >> 9) | (a.v[4] << 20);
+  w[4] = (a.v[4] >> 12) | (a.v[5] << 17);
+  w[5] = (a.v[5] >> 15) | (a.v[6] << 14);
+  w[6] = (a.v[6] >> 18) | (a.v[7] << 11);
+  w[7] = (a.v[7] >> 21) | (a.v[8] << 8);
+}
+
+template <class P>
+ZK_HD Fe fe_const(const uint32_t (&c)[NL]) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = c[i];
+  return r;
+}
+ZK_HD Fe fe_zero() {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = 0;
+  return r;
+}
+
+// ------------------------------------------------------------ Montgomery mul
+// r = a*b*2^-261 mod p (lazy: result < 2p, normalised limbs).
+template <class P>
+ZK_HD Fe mul(const Fe& a, const Fe& b) {
+  uint32_t m[NL];
+  Fe r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      acc += (uint64_t)a.v[j] * b.v[k - j];
+      acc += (uint64_t)m[j] * P::P[k - j];
+    }
+    acc += (uint64_t)a.v[k] * b.v[0];
+    m[k] = ((uint32_t)acc * P::PINV) & LMASK;
+    acc += (uint64_t)m[k] * P::P[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) {
+      acc += (uint64_t)a.v[j] * b.v[k - j];
+      acc += (uint64_t)m[j] * P::P[k - j];
+    }
+    r.v[k - NL] = (uint32_t)acc & LMASK;
+    acc >>= 29;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+// squaring: off-diagonal products once, doubled operand
+template <class P>
+ZK_HD Fe sqr(const Fe& a) {
+  uint32_t m[NL], d[NL];
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) d[i] = a.v[i] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int j = 0; j < (k + 1) / 2; j++) acc += (uint64_t)d[j] * a.v[k - j];
+    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+#pragma unroll
+    for (int j = 0; j < k; j++) acc += (uint64_t)m[j] * P::P[k - j];
+    m[k] = ((uint32_t)acc * P::PINV) & LMASK;
+    acc += (uint64_t)m[k] * P::P[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) acc += (uint64_t)d[j] * a.v[k - j];
+    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) acc += (uint64_t)m[j] * P::P[k - j];
+    r.v[k - NL] = (uint32_t)acc & LMASK;
+    acc >>= 29;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+// --------------------------------------------------------------- add / sub
+// r = a - b mod p for a, b in [0, 2p) normalised -> [0, 2p) normalised.
+template <class P>
+ZK_HD Fe sub(const Fe& a, const Fe& b) {
+  Fe r;
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    int32_t t = (int32_t)a.v[i] - (int32_t)b.v[i] + br;
+    r.v[i] = (uint32_t)t & LMASK;
+    br = t >> 29;
+  }
+  // br is 0 or -1; add 2p under mask
+  uint32_t mask = (uint32_t)br;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    uint32_t t = r.v[i] + (P::P2[i] & mask) + c;
+    r.v[i] = t & LMASK;
+    c = t >> 29;
+  }
+  return r;
+}
+// r = a + b mod p for a, b in [0, 2p) -> [0, 2p)
+template <class P>
+ZK_HD Fe add(const Fe& a, const Fe& b) {
+  Fe r;
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    int32_t t = (int32_t)(a.v[i] + b.v[i]) - (int32_t)P::P2[i] + br;
+    r.v[i] = (uint32_t)t & LMASK;
+    br = t >> 29;
+  }
+  uint32_t mask = (uint32_t)(br >> 31);  // top is negative -> add 2p back
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    uint32_t t = r.v[i] + (P::P2[i] & mask) + c;
+    r.v[i] = t & LMASK;
+    c = t >> 29;
+  }
+  return r;
+}
+template <class P>
+ZK_HD Fe dbl(const Fe& a) {
+  return add<P>(a, a);
+}
+template <class P>
+ZK_HD Fe neg(const Fe& a) {
+  return sub<P>(fe_zero(), a);
+}
+// lazy add: limbwise, no carry (limbs < 2^30, value < 4p).  Only as a mul input.
+ZK_HD Fe add_lazy(const Fe& a, const Fe& b) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = a.v[i] + b.v[i];
+  return r;
+}
+
+// fully reduce [0, 2p) -> [0, p)
+template <class P>
+ZK_HD Fe reduce(const Fe& a) {
+  Fe d;
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    int32_t t = (int32_t)a.v[i] - (int32_t)P::P[i] + br;
+    d.v[i] = (uint32_t)t & LMASK;
+    br = t >> 29;
+  }
+  Fe r;
+  bool neg_ = br < 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = neg_ ? a.v[i] : d.v[i];
+  return r;
+}
+template <class P>
+ZK_HD bool is_zero(const Fe& a) {
+  Fe t = reduce<P>(a);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) o |= t.v[i];
+  return o == 0;
+}
+template <class P>
+ZK_HD bool eq(const Fe& a, const Fe& b) {
+  Fe x = reduce<P>(a), y = reduce<P>(b);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) o |= x.v[i] ^ y.v[i];
+  return o == 0;
+}
+template <class P>
+ZK_HD Fe one() {
+  return fe_const<P>(P::ONE);
+}
+// canonical (packed, < p) -> Montgomery internal
+template <class P>
+ZK_HD Fe to_mont(const Fe& a) {
+  return mul<P>(a, fe_const<P>(P::R2));
+}
+// Montgomery internal -> canonical, fully reduced
+template <class P>
+ZK_HD Fe from_mont(const Fe& a) {
+  Fe o = fe_zero();
+  o.v[0] = 1;
+  return reduce<P>(mul<P>(a, o));
+}
+// a^e for a small public exponent given as 4 x u64 (used off the hot path)
+template <class P>
+ZK_HD Fe pow(const Fe& a, const uint64_t e[4]) {
+  Fe r = one<P>();
+  for (int i = 255; i >= 0; i--) {
+    r = sqr<P>(r);
+    if ((e[i >> 6] >> (i & 63)) & 1) r = mul<P>(r, a);
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- Fq2
+// Fq2 = Fq[u]/(u^2 + 1)
+struct Fe2 {
+  Fe c0, c1;
+};
+ZK_HD Fe2 f2_add(const Fe2& a, const Fe2& b) { return {add<FqP>(a.c0, b.c0), add<FqP>(a.c1, b.c1)}; }
+ZK_HD Fe2 f2_sub(const Fe2& a, const Fe2& b) { return {sub<FqP>(a.c0, b.c0), sub<FqP>(a.c1, b.c1)}; }
+ZK_HD Fe2 f2_dbl(const Fe2& a) { return {dbl<FqP>(a.c0), dbl<FqP>(a.c1)}; }
+ZK_HD Fe2 f2_neg(const Fe2& a) { return {neg<FqP>(a.c0), neg<FqP>(a.c1)}; }
+ZK_HD Fe2 f2_mul(const Fe2& a, const Fe2& b) {
+  Fe t0 = mul<FqP>(a.c0, b.c0);
+  Fe t1 = mul<FqP>(a.c1, b.c1);
+  Fe t2 = mul<FqP>(add_lazy(a.c0, a.c1), add_lazy(b.c0, b.c1));
+  return {sub<FqP>(t0, t1), sub<FqP>(sub<FqP>(t2, t0), t1)};
+}
+ZK_HD Fe2 f2_sqr(const Fe2& a) {
+  // (a0 + a1 u)^2 = (a0+a1)(a0-a1) + 2 a0 a1 u
+  Fe s = add_lazy(a.c0, a.c1);
+  Fe d = sub<FqP>(a.c0, a.c1);
+  Fe c0 = mul<FqP>(s, d);
+  Fe c1 = mul<FqP>(a.c0, a.c1);
+  return {c0, dbl<FqP>(c1)};
+}
+ZK_HD bool f2_is_zero(const Fe2& a) { return is_zero<FqP>(a.c0) && is_zero<FqP>(a.c1); }
+ZK_HD bool fe_is_zero_raw(const Fe& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) o |= a.v[i];
+  return o == 0;
+}
+ZK_HD Fe2 f2_zero() { return {fe_zero(), fe_zero()}; }
+ZK_HD Fe2 f2_one() { return {one<FqP>(), fe_zero()}; }
+
+// Uniform field interface used by the curve templates.
+struct FqOps {
+  using T = Fe;
+  static ZK_HD T mul(const T& a, const T& b) { return zk::mul<FqP>(a, b); }
+  static ZK_HD T sqr(const T& a) { return zk::sqr<FqP>(a); }
+  static ZK_HD T add(const T& a, const T& b) { return zk::add<FqP>(a, b); }
+  static ZK_HD T sub(const T& a, const T& b) { return zk::sub<FqP>(a, b); }
+  static ZK_HD T dbl(const T& a) { return zk::dbl<FqP>(a); }
+  static ZK_HD T neg(const T& a) { return zk::neg<FqP>(a); }
+  static ZK_HD bool is_zero(const T& a) { return zk::is_zero<FqP>(a); }
+  static ZK_HD bool is_zero_raw(const T& a) { return fe_is_zero_raw(a); }
+  static ZK_HD T zero() { return fe_zero(); }
+  static ZK_HD T one() { return zk::one<FqP>(); }
+};
+struct Fq2Ops {
+  using T = Fe2;
+  static ZK_HD T mul(const T& a, const T& b) { return f2_mul(a, b); }
+  static ZK_HD T sqr(const T& a) { return f2_sqr(a); }
+  static ZK_HD T add(const T& a, const T& b) { return f2_add(a, b); }
+  static ZK_HD T sub(const T& a, const T& b) { return f2_sub(a, b); }
+  static ZK_HD T dbl(const T& a) { return f2_dbl(a); }
+  static ZK_HD T neg(const T& a) { return f2_neg(a); }
+  static ZK_HD bool is_zero(const T& a) { return f2_is_zero(a); }
+  static ZK_HD bool is_zero_raw(const T& a) { return fe_is_zero_raw(a.c0) && fe_is_zero_raw(a.c1); }
+  static ZK_HD T zero() { return f2_zero(); }
+  static ZK_HD T one() { return f2_one(); }
+};
+
+}  // namespace zk

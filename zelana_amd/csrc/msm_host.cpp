@@ -1,0 +1,178 @@
+// msm_host.cpp — host epilogue of the GPU MSM and host-side point encodings.
+//
+// The GPU hands over ~c*W + W canonical XYZZ bit sums; the remaining work is a
+// single strictly sequential Horner chain (~255 doublings) that a CPU core
+// finishes in ~30-60 us while one GPU lane would need ~1 ms (one XYZZ doubling
+// is ~2k dependent VALU ops).  Also: affine conversion, the arkworks SWFlags
+// point encodings and the 256-B Solana proof layout of
+// core/src/sequencer/settlement/prover.rs:304-334.
+#include <stdint.h>
+#include <string.h>
+
+#include "host_field.h"
+#include "zkmi_internal_host.h"
+
+using namespace zkh;
+
+namespace {
+
+template <class F>
+using HX = zk::Xyzz<F>;
+
+F4 ld_canon32(const uint32_t* w) {
+  uint64_t c[4];
+  for (int i = 0; i < 4; i++) c[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+  return from_canon(c);
+}
+template <class F>
+typename F::T ld_coord(const uint32_t* w);
+template <>
+F4 ld_coord<HFq>(const uint32_t* w) {
+  return ld_canon32(w);
+}
+template <>
+F42 ld_coord<HFq2>(const uint32_t* w) {
+  return {ld_canon32(w), ld_canon32(w + 8)};
+}
+template <class F, int CW>
+HX<F> ld_term(const uint32_t* p) {
+  HX<F> r;
+  r.x = ld_coord<F>(p);
+  r.y = ld_coord<F>(p + CW);
+  r.zz = ld_coord<F>(p + 2 * CW);
+  r.zzz = ld_coord<F>(p + 3 * CW);
+  return r;
+}
+
+F4 inv1(const F4& a) { return finv(a); }
+F42 inv1(const F42& a) { return HFq2::inv(a); }
+void put(uint64_t* o, const F4& a) { to_canon(o, a); }
+void put(uint64_t* o, const F42& a) {
+  to_canon(o, a.c0);
+  to_canon(o + 4, a.c1);
+}
+
+template <class F, int CW>
+void to_affine(const HX<F>& p, uint64_t* out) {
+  const int K = CW / 8 * 4;  // u64 per coordinate
+  if (zk::xyzz_is_inf(p)) {
+    memset(out, 0, 2 * K * 8);
+    return;
+  }
+  // x = X / ZZ, y = Y / ZZZ
+  typename F::T izz = inv1(p.zz), izzz = inv1(p.zzz);
+  put(out, F::mul(p.x, izz));
+  put(out + K, F::mul(p.y, izzz));
+}
+
+template <class F, int CW>
+void combine(const uint32_t* terms, int nbits, int W, int c, uint64_t* out) {
+  constexpr int XW = 4 * CW;
+  HX<F> acc = zk::xyzz_inf<F>();
+  for (int k = nbits - 1; k >= 0; k--) {
+    acc = zk::xyzz_dbl(acc);
+    acc = zk::xyzz_add(acc, ld_term<F, CW>(terms + (size_t)k * XW));
+    if (k % c == 0) acc = zk::xyzz_add(acc, ld_term<F, CW>(terms + (size_t)(nbits + k / c) * XW));
+  }
+  (void)W;
+  to_affine<F, CW>(acc, out);
+}
+
+template <class F, int K>
+HX<F> from_aff_canon(const uint64_t* a) {
+  bool z = true;
+  for (int i = 0; i < 2 * K; i++) z &= a[i] == 0;
+  if (z) return zk::xyzz_inf<F>();
+  zk::Aff<F> p;
+  uint32_t w[16];
+  (void)w;
+  if constexpr (K == 4) {
+    p.x = from_canon(a);
+    p.y = from_canon(a + 4);
+  } else {
+    p.x = {from_canon(a), from_canon(a + 4)};
+    p.y = {from_canon(a + 8), from_canon(a + 12)};
+  }
+  return zk::xyzz_from_aff(p);
+}
+
+}  // namespace
+
+namespace zk {
+void msm_host_combine_g1(const uint32_t* terms, int nbits, int W, int c, uint64_t out[8]) {
+  combine<HFq, 8>(terms, nbits, W, c, out);
+}
+void msm_host_combine_g2(const uint32_t* terms, int nbits, int W, int c, uint64_t out[16]) {
+  combine<HFq2, 16>(terms, nbits, W, c, out);
+}
+void host_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {
+  auto r = xyzz_add(from_aff_canon<HFq, 4>(a), from_aff_canon<HFq, 4>(b));
+  to_affine<HFq, 8>(r, out);
+}
+void host_g2_add_affine(const uint64_t a[16], const uint64_t b[16], uint64_t out[16]) {
+  auto r = xyzz_add(from_aff_canon<HFq2, 8>(a), from_aff_canon<HFq2, 8>(b));
+  to_affine<HFq2, 16>(r, out);
+}
+
+// ---------------------------------------------------------- encodings
+static void put_le(uint8_t* o, const uint64_t c[4]) {
+  for (int i = 0; i < 32; i++) o[i] = (uint8_t)(c[i / 8] >> (8 * (i % 8)));
+}
+static int cmp_canon(const uint64_t a[4], const uint64_t b[4]) {
+  for (int i = 3; i >= 0; i--) {
+    if (a[i] != b[i]) return a[i] > b[i] ? 1 : -1;
+  }
+  return 0;
+}
+static void neg_canon(uint64_t o[4], const uint64_t a[4]) {
+  if ((a[0] | a[1] | a[2] | a[3]) == 0) {
+    memset(o, 0, 32);
+    return;
+  }
+  sub4(o, QP, a);
+}
+// arkworks SWFlags: bit 7 of the last byte = y > -y, bit 6 = infinity
+void g1_compress(const uint64_t p[8], uint8_t out[32]) {
+  bool inf = true;
+  for (int i = 0; i < 8; i++) inf &= p[i] == 0;
+  memset(out, 0, 32);
+  if (inf) {
+    out[31] |= 0x40;
+    return;
+  }
+  put_le(out, p);
+  uint64_t ny[4];
+  neg_canon(ny, p + 4);
+  if (cmp_canon(p + 4, ny) > 0) out[31] |= 0x80;
+}
+void g2_compress(const uint64_t p[16], uint8_t out[64]) {
+  bool inf = true;
+  for (int i = 0; i < 16; i++) inf &= p[i] == 0;
+  memset(out, 0, 64);
+  if (inf) {
+    out[63] |= 0x40;
+    return;
+  }
+  put_le(out, p);
+  put_le(out + 32, p + 4);
+  // Fq2 order: c1 first, then c0
+  uint64_t n0[4], n1[4];
+  neg_canon(n0, p + 8);
+  neg_canon(n1, p + 12);
+  int c = cmp_canon(p + 12, n1);
+  if (c == 0) c = cmp_canon(p + 8, n0);
+  if (c > 0) out[63] |= 0x80;
+}
+void proof_solana(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8], uint8_t out[256]) {
+  uint64_t ny[4];
+  neg_canon(ny, a + 4);
+  put_le(out, a);       // -A: x unchanged
+  put_le(out + 32, ny); //      y negated
+  put_le(out + 64, b);
+  put_le(out + 96, b + 4);
+  put_le(out + 128, b + 8);
+  put_le(out + 160, b + 12);
+  put_le(out + 192, c);
+  put_le(out + 224, c + 4);
+}
+}  // namespace zk

@@ -1,0 +1,277 @@
+// zkmi_api.hip — the extern "C" boundary of libzkmi.so (include/zkmi.h):
+// context / device memory, kernel timing, MSM and NTT entry points, encodings.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "zkmi_internal.h"
+
+namespace zk {
+
+static thread_local char g_err[512] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int Workspace::get(const char* name, size_t bytes, void** out) {
+  auto it = bufs.find(name);
+  if (it != bufs.end() && it->second.second >= bytes) {
+    *out = it->second.first;
+    return 0;
+  }
+  if (it != bufs.end()) {
+    hipFree(it->second.first);
+    bufs.erase(it);
+  }
+  void* p = nullptr;
+  size_t sz = bytes < 256 ? 256 : bytes;
+  if (hipMalloc(&p, sz) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("workspace '%s': hipMalloc(%zu) failed", name, sz);
+    return ZKMI_ENOMEM;
+  }
+  bufs[name] = {p, sz};
+  *out = p;
+  return 0;
+}
+void Workspace::release_all() {
+  for (auto& kv : bufs) hipFree(kv.second.first);
+  bufs.clear();
+}
+
+void timer_begin(zkmi_ctx* ctx, const char* name, hipEvent_t* ev) {
+  *ev = nullptr;
+  if (!ctx->timer.enabled) return;
+  if (hipEventCreate(ev) != hipSuccess) {
+    *ev = nullptr;
+    return;
+  }
+  hipEventRecord(*ev, ctx->stream);
+}
+void timer_end(zkmi_ctx* ctx, const char* name, hipEvent_t ev) {
+  if (!ctx->timer.enabled || !ev) return;
+  hipEvent_t e2;
+  if (hipEventCreate(&e2) != hipSuccess) return;
+  hipEventRecord(e2, ctx->stream);
+  ctx->timer.pending.push_back({ev, e2, name});
+}
+int timer_flush(zkmi_ctx* ctx) {
+  if (ctx->timer.pending.empty()) return 0;
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  for (auto& r : ctx->timer.pending) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, r.a, r.b);
+    auto& t = ctx->timer.totals[r.name];
+    t.first += ms;
+    t.second += 1;
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
+  ctx->timer.pending.clear();
+  return 0;
+}
+
+}  // namespace zk
+
+using namespace zk;
+
+extern "C" {
+
+const char* zkmi_last_error(void) { return g_err; }
+int zkmi_version(void) { return 1; }
+
+int zkmi_ctx_create(int device, zkmi_ctx** out) {
+  if (!out) {
+    set_error("zkmi_ctx_create: null out");
+    return ZKMI_EINVAL;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    (void)hipGetLastError();
+    set_error("no HIP device available (libzkmi has no CPU fallback)");
+    return ZKMI_ENODEV;
+  }
+  if (device < 0 || device >= ndev) {
+    set_error("device %d out of range (%d devices)", device, ndev);
+    return ZKMI_ENODEV;
+  }
+  hipDeviceProp_t prop;
+  ZK_HIP(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_error("device %d is %s; libzkmi is built for gfx950 (MI355X) only", device, prop.gcnArchName);
+    return ZKMI_ENODEV;
+  }
+  ZK_HIP(hipSetDevice(device));
+  zkmi_ctx* c = new zkmi_ctx;
+  c->device = device;
+  c->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    set_error("hipStreamCreate failed");
+    return ZKMI_EHIP;
+  }
+  *out = c;
+  return 0;
+}
+void zkmi_ctx_destroy(zkmi_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  timer_flush(ctx);
+  ctx->ws.release_all();
+  hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+int zkmi_profile_enable(zkmi_ctx* ctx, int on) {
+  ctx->timer.enabled = on != 0;
+  return 0;
+}
+int zkmi_profile_get(zkmi_ctx* ctx, const char* name, double* total_ms, uint64_t* count) {
+  ZK_TRY(timer_flush(ctx));
+  auto it = ctx->timer.totals.find(name);
+  *total_ms = it == ctx->timer.totals.end() ? 0.0 : it->second.first;
+  *count = it == ctx->timer.totals.end() ? 0 : it->second.second;
+  return 0;
+}
+int zkmi_profile_reset(zkmi_ctx* ctx) {
+  ZK_TRY(timer_flush(ctx));
+  ctx->timer.totals.clear();
+  return 0;
+}
+int zkmi_dev_alloc(zkmi_ctx* ctx, size_t bytes, void** dptr) {
+  hipSetDevice(ctx->device);
+  if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("hipMalloc(%zu) failed", bytes);
+    return ZKMI_ENOMEM;
+  }
+  return 0;
+}
+int zkmi_dev_free(zkmi_ctx* ctx, void* dptr) {
+  (void)ctx;
+  ZK_HIP(hipFree(dptr));
+  return 0;
+}
+int zkmi_h2d(zkmi_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  ZK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+int zkmi_d2h(zkmi_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  ZK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+int zkmi_sync(zkmi_ctx* ctx) {
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+// ------------------------------------------------------------------ MSM
+int zkmi_bases_create_g1(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_bases** out) {
+  return bases_upload(ctx, 0, affine, n, out);
+}
+int zkmi_bases_create_g2(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_bases** out) {
+  return bases_upload(ctx, 1, affine, n, out);
+}
+void zkmi_bases_destroy(zkmi_bases* b) {
+  if (!b) return;
+  hipFree(b->d_pts);
+  delete b;
+}
+size_t zkmi_bases_len(const zkmi_bases* b) { return b ? b->n : 0; }
+
+static int msm_host_scalars(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_t* scalars, size_t n,
+                            uint64_t* out) {
+  void* d;
+  ZK_TRY(ctx->ws.get("msm_scalars_stage", n * 32 + 32, &d));
+  if (n) ZK_HIP(hipMemcpyAsync(d, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  return msm_device(ctx, b, offset, d, n, out);
+}
+int zkmi_msm_g1(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_t* scalars, size_t n,
+                uint64_t out_affine[8]) {
+  if (!b || b->g2) {
+    set_error("zkmi_msm_g1: G1 base set required");
+    return ZKMI_EINVAL;
+  }
+  return msm_host_scalars(ctx, b, offset, scalars, n, out_affine);
+}
+int zkmi_msm_g2(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_t* scalars, size_t n,
+                uint64_t out_affine[16]) {
+  if (!b || !b->g2) {
+    set_error("zkmi_msm_g2: G2 base set required");
+    return ZKMI_EINVAL;
+  }
+  return msm_host_scalars(ctx, b, offset, scalars, n, out_affine);
+}
+int zkmi_msm_g1_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+                       uint64_t out_affine[8]) {
+  if (!b || b->g2) {
+    set_error("zkmi_msm_g1_device: G1 base set required");
+    return ZKMI_EINVAL;
+  }
+  return msm_device(ctx, b, offset, d_scalars, n, out_affine);
+}
+int zkmi_msm_g2_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+                       uint64_t out_affine[16]) {
+  if (!b || !b->g2) {
+    set_error("zkmi_msm_g2_device: G2 base set required");
+    return ZKMI_EINVAL;
+  }
+  return msm_device(ctx, b, offset, d_scalars, n, out_affine);
+}
+int zkmi_msm_set_window(zkmi_ctx* ctx, int c) {
+  if (c != 0 && (c < 4 || c > 17)) {
+    set_error("window %d outside [4, 17]", c);
+    return ZKMI_EINVAL;
+  }
+  ctx->msm_window = c;
+  return 0;
+}
+int zkmi_g1_add(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {
+  host_g1_add_affine(a, b, out);
+  return 0;
+}
+int zkmi_g2_add(const uint64_t a[16], const uint64_t b[16], uint64_t out[16]) {
+  host_g2_add_affine(a, b, out);
+  return 0;
+}
+
+// ------------------------------------------------------------------ NTT
+int zkmi_ntt_device(zkmi_ctx* ctx, void* d_data, uint32_t log_n, int inverse, int coset) {
+  ZK_TRY(ntt_device(ctx, (uint32_t*)d_data, log_n, inverse, coset));
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  return timer_flush(ctx);
+}
+int zkmi_ntt(zkmi_ctx* ctx, uint64_t* data, uint32_t log_n, int inverse, int coset) {
+  if (log_n > 28) {
+    set_error("ntt: log_n %u > 28", log_n);
+    return ZKMI_EINVAL;
+  }
+  size_t bytes = ((size_t)1 << log_n) * 32;
+  void* d;
+  ZK_TRY(ctx->ws.get("ntt_stage", bytes, &d));
+  ZK_HIP(hipMemcpyAsync(d, data, bytes, hipMemcpyHostToDevice, ctx->stream));
+  ZK_TRY(ntt_device(ctx, (uint32_t*)d, log_n, inverse, coset));
+  ZK_HIP(hipMemcpyAsync(data, d, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  return timer_flush(ctx);
+}
+
+// ------------------------------------------------------------- encodings
+int zkmi_proof_to_solana_bytes(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8], uint8_t out[256]) {
+  proof_solana(a, b, c, out);
+  return 0;
+}
+int zkmi_proof_serialize_compressed(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8],
+                                    uint8_t out[128]) {
+  g1_compress(a, out);
+  g2_compress(b, out + 32);
+  g1_compress(c, out + 96);
+  return 0;
+}
+
+}  // extern "C"

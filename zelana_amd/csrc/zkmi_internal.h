@@ -1,0 +1,92 @@
+// zkmi_internal.h — context, error plumbing, workspace and kernel timing shared
+// by the HIP translation units of libzkmi.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/zkmi.h"
+#include "zkmi_internal_host.h"
+
+namespace zk {
+
+void set_error(const char* fmt, ...);
+
+#define ZK_HIP(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) {                                                                \
+      ::zk::set_error("HIP error %s at %s:%d (%s)", hipGetErrorString(e_), __FILE__, __LINE__, #expr); \
+      return ZKMI_EHIP;                                                                    \
+    }                                                                                      \
+  } while (0)
+
+#define ZK_TRY(expr)          \
+  do {                        \
+    int rc_ = (expr);         \
+    if (rc_ != 0) return rc_; \
+  } while (0)
+
+// grow-only device scratch buffers keyed by name
+struct Workspace {
+  std::map<std::string, std::pair<void*, size_t>> bufs;
+  int get(const char* name, size_t bytes, void** out);
+  void release_all();
+};
+
+struct KernelTimer {
+  bool enabled = false;
+  struct Rec {
+    hipEvent_t a, b;
+    std::string name;
+  };
+  std::vector<Rec> pending;
+  std::map<std::string, std::pair<double, uint64_t>> totals;
+};
+
+}  // namespace zk
+
+struct zkmi_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  zk::Workspace ws;
+  zk::KernelTimer timer;
+  int msm_window = 0;  // 0 = auto
+  int num_cus = 256;
+};
+
+struct zkmi_bases {
+  zkmi_ctx* ctx;
+  int g2;           // 0 = G1 (16 words / point), 1 = G2 (32 words / point)
+  size_t n;
+  uint32_t* d_pts;  // packed affine, internal Montgomery, inf flag = bit 31 of last word
+};
+
+namespace zk {
+// kernel timing helpers (events on ctx->stream)
+void timer_begin(zkmi_ctx* ctx, const char* name, hipEvent_t* ev);
+void timer_end(zkmi_ctx* ctx, const char* name, hipEvent_t ev);
+int timer_flush(zkmi_ctx* ctx);
+
+struct ScopedKernelTimer {
+  zkmi_ctx* ctx;
+  const char* name;
+  hipEvent_t ev = nullptr;
+  ScopedKernelTimer(zkmi_ctx* c, const char* n) : ctx(c), name(n) { timer_begin(ctx, name, &ev); }
+  ~ScopedKernelTimer() { timer_end(ctx, name, ev); }
+};
+
+// MSM entry (msm.hip): device scalars, result canonical affine
+int msm_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+               uint64_t* out_affine);
+int bases_upload(zkmi_ctx* ctx, int g2, const uint64_t* host_affine, size_t n, zkmi_bases** out);
+// convert canonical affine already in device memory (n points) into a bases set
+int bases_from_device_canon(zkmi_ctx* ctx, int g2, const uint32_t* d_canon, size_t n, zkmi_bases** out);
+
+// NTT entry (ntt.hip): in-place on device, natural order
+int ntt_device(zkmi_ctx* ctx, uint32_t* d_data, uint32_t log_n, int inverse, int coset);
+
+}  // namespace zk

@@ -1,0 +1,18 @@
+// zkmi_internal_host.h — host-only helpers of libzkmi.so (no HIP dependency;
+// compiled by g++ in msm_host.cpp).
+#pragma once
+#include <stdint.h>
+
+namespace zk {
+// MSM epilogue: terms[k] (k < nbits) = canonical packed XYZZ of weight 2^k;
+// terms[nbits + w] (w < W) = window total T_w of weight 2^(c w).  Result is
+// canonical affine (all-zero = infinity).
+void msm_host_combine_g1(const uint32_t* terms, int nbits, int W, int c, uint64_t out[8]);
+void msm_host_combine_g2(const uint32_t* terms, int nbits, int W, int c, uint64_t out[16]);
+void host_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
+void host_g2_add_affine(const uint64_t a[16], const uint64_t b[16], uint64_t out[16]);
+// arkworks compressed encodings and the Solana 256-byte proof layout
+void g1_compress(const uint64_t p[8], uint8_t out[32]);
+void g2_compress(const uint64_t p[16], uint8_t out[64]);
+void proof_solana(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8], uint8_t out[256]);
+}  // namespace zk

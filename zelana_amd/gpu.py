@@ -1,0 +1,147 @@
+"""Thin Python handle over libzkmi.so for device-resident MSM / NTT / Groth16.
+
+Arrays cross as numpy uint64 (canonical little-endian limbs), matching the C
+ABI.  One Context per GPU (one process per GPU, see bench.py).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import R1CSStruct, ZkmiError, check, lib, u64p, u8p, vp
+
+
+def _p64(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags.c_contiguous
+    return a.ctypes.data_as(u64p)
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx, self.nbytes = ctx, nbytes
+        self.ptr = vp()
+        check(lib().zkmi_dev_alloc(ctx.h, nbytes, ctypes.byref(self.ptr)), "zkmi_dev_alloc")
+
+    def upload(self, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        check(lib().zkmi_h2d(self.ctx.h, self.ptr, arr.ctypes.data_as(vp), arr.nbytes), "zkmi_h2d")
+
+    def download(self, arr: np.ndarray):
+        assert arr.flags.c_contiguous and arr.nbytes <= self.nbytes
+        check(lib().zkmi_d2h(self.ctx.h, arr.ctypes.data_as(vp), self.ptr, arr.nbytes), "zkmi_d2h")
+        return arr
+
+    def free(self):
+        if self.ptr:
+            lib().zkmi_dev_free(self.ctx.h, self.ptr)
+            self.ptr = vp()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Bases:
+    def __init__(self, ctx: "Context", points: np.ndarray, g2: bool):
+        pts = np.ascontiguousarray(points, dtype=np.uint64)
+        assert pts.ndim == 2 and pts.shape[1] == (16 if g2 else 8)
+        self.ctx, self.g2, self.n = ctx, g2, pts.shape[0]
+        self.h = vp()
+        f = lib().zkmi_bases_create_g2 if g2 else lib().zkmi_bases_create_g1
+        check(f(ctx.h, _p64(pts), self.n, ctypes.byref(self.h)), "zkmi_bases_create")
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().zkmi_bases_destroy(self.h)
+                self.h = vp()
+        except Exception:
+            pass
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        self.h = vp()
+        check(lib().zkmi_ctx_create(device, ctypes.byref(self.h)), "zkmi_ctx_create")
+
+    def close(self):
+        if self.h:
+            lib().zkmi_ctx_destroy(self.h)
+            self.h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- timing
+    def profile(self, on: bool = True):
+        check(lib().zkmi_profile_enable(self.h, int(on)))
+
+    def profile_get(self, name: str):
+        t, c = ctypes.c_double(), ctypes.c_uint64()
+        check(lib().zkmi_profile_get(self.h, name.encode(), ctypes.byref(t), ctypes.byref(c)))
+        return t.value, c.value
+
+    def profile_reset(self):
+        check(lib().zkmi_profile_reset(self.h))
+
+    def set_window(self, c: int):
+        check(lib().zkmi_msm_set_window(self.h, c))
+
+    def sync(self):
+        check(lib().zkmi_sync(self.h))
+
+    # --- MSM
+    def bases_g1(self, points):
+        return Bases(self, points, False)
+
+    def bases_g2(self, points):
+        return Bases(self, points, True)
+
+    def msm(self, bases: Bases, scalars, offset: int = 0):
+        out = np.zeros(16 if bases.g2 else 8, np.uint64)
+        if isinstance(scalars, DeviceBuffer):
+            n = scalars.nbytes // 32
+            f = lib().zkmi_msm_g2_device if bases.g2 else lib().zkmi_msm_g1_device
+            check(f(self.h, bases.h, offset, scalars.ptr, n, _p64(out)), "zkmi_msm_device")
+        else:
+            sc = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+            f = lib().zkmi_msm_g2 if bases.g2 else lib().zkmi_msm_g1
+            check(f(self.h, bases.h, offset, _p64(sc), sc.shape[0], _p64(out)), "zkmi_msm")
+        return out
+
+    def msm_device_n(self, bases: Bases, dscalars: DeviceBuffer, n: int, offset: int = 0):
+        out = np.zeros(16 if bases.g2 else 8, np.uint64)
+        f = lib().zkmi_msm_g2_device if bases.g2 else lib().zkmi_msm_g1_device
+        check(f(self.h, bases.h, offset, dscalars.ptr, n, _p64(out)), "zkmi_msm_device")
+        return out
+
+    # --- NTT
+    def ntt(self, data: np.ndarray, log_n: int, inverse=False, coset=False):
+        d = np.ascontiguousarray(data, dtype=np.uint64).copy()
+        assert d.size == 4 << log_n
+        check(lib().zkmi_ntt(self.h, _p64(d), log_n, int(inverse), int(coset)), "zkmi_ntt")
+        return d.reshape(-1, 4)
+
+    def ntt_device(self, buf: DeviceBuffer, log_n: int, inverse=False, coset=False):
+        check(lib().zkmi_ntt_device(self.h, buf.ptr, log_n, int(inverse), int(coset)), "zkmi_ntt_device")
+
+
+def g1_add(a, b):
+    out = np.zeros(8, np.uint64)
+    check(lib().zkmi_g1_add(_p64(np.ascontiguousarray(a, np.uint64)), _p64(np.ascontiguousarray(b, np.uint64)),
+                            _p64(out)))
+    return out
+
+
+def g2_add(a, b):
+    out = np.zeros(16, np.uint64)
+    check(lib().zkmi_g2_add(_p64(np.ascontiguousarray(a, np.uint64)), _p64(np.ascontiguousarray(b, np.uint64)),
+                            _p64(out)))
+    return out
