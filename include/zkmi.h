@@ -51,6 +51,7 @@ extern "C" {
 typedef struct zkmi_ctx zkmi_ctx;
 typedef struct zkmi_bases zkmi_bases;
 typedef struct zkmi_pk zkmi_pk;
+typedef struct zkmi_msm_job zkmi_msm_job;
 
 const char* zkmi_last_error(void);
 int zkmi_version(void);
@@ -77,6 +78,14 @@ int zkmi_bases_create_g1(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_b
 int zkmi_bases_create_g2(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_bases** out);
 void zkmi_bases_destroy(zkmi_bases* b);
 size_t zkmi_bases_len(const zkmi_bases* b);
+/* canonical affine copy of a base set (n x 8 or n x 16 u64) */
+int zkmi_bases_export(const zkmi_bases* b, uint64_t* affine_out);
+/* Deterministic synthetic inputs generated directly in HBM (benchmarks):
+ * bases P_i = k_i * G (k_i from a splitmix64 stream of seed), scalars uniform
+ * in [0, r) by rejection.  d_scalars must hold n x 32 bytes. */
+int zkmi_bases_generate_g1(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** out);
+int zkmi_bases_generate_g2(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** out);
+int zkmi_scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_scalars);
 
 /* sum_{i<n} scalars[i] * bases[offset + i]; n <= len - offset.
  * Host scalars (n x 4 u64). Result: canonical affine. */
@@ -89,6 +98,14 @@ int zkmi_msm_g1_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const 
                        uint64_t out_affine[8]);
 int zkmi_msm_g2_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                        uint64_t out_affine[16]);
+/* Asynchronous form: submit queues the GPU work (and the copy of the ~c*W
+ * window bit-sums) on the context stream and returns at once; wait finishes
+ * the O(windows) host epilogue and frees the job.  Submitting MSM k+1 before
+ * waiting on MSM k overlaps k's epilogue with k+1's kernels.  Scalars must
+ * stay valid until wait returns. */
+int zkmi_msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+                    zkmi_msm_job** job);
+int zkmi_msm_wait(zkmi_msm_job* job, uint64_t* out_affine);
 /* window size override for experiments (0 = automatic) */
 int zkmi_msm_set_window(zkmi_ctx* ctx, int c);
 

@@ -139,3 +139,34 @@ def test_ntt_roundtrip_2pow20(ctx):
     delta = ctx.ntt(one, log_n)  # NTT of delta_0 = all ones
     assert np.all(delta[:, 0] == 1) and np.all(delta[:, 1:] == 0)
     assert not np.array_equal(f2, data)
+
+
+def test_generated_inputs(ctx):
+    """Device-generated synthetic bases are on the curve (checked by the
+    oracle), exported canonically, and the MSM over them matches the oracle."""
+    n = 5000
+    b = ctx.bases_generate(seed=7, n=n)
+    pts = b.export()
+    assert all(O.lib().oracle_g1_on_curve(O.P(np.ascontiguousarray(p))) for p in pts[:64])
+    d = ctx.scalars_generate(seed=3, n=n)
+    sc = np.zeros((n, 4), np.uint64)
+    d.download(sc)
+    assert all(O.limbs_to_int(s) < O.R for s in sc)
+    assert np.array_equal(ctx.msm(b, d), O.msm_g1(pts, sc))
+    b2 = ctx.bases_generate(seed=9, n=64, g2=True)
+    p2 = b2.export()
+    assert all(O.lib().oracle_g2_on_curve(O.P(np.ascontiguousarray(p))) for p in p2)
+    assert np.array_equal(ctx.msm(b2, sc[:64]), O.msm_g2(p2, sc[:64]))
+
+
+def test_msm_pipelined(ctx):
+    n = 20000
+    b = ctx.bases_generate(seed=11, n=n)
+    d = ctx.scalars_generate(seed=12, n=n)
+    want = ctx.msm(b, d)
+    jobs = [ctx.msm_submit(b, d, n), ctx.msm_submit(b, d, n - 1000, 0)]
+    r0, r1 = ctx.msm_wait(jobs[0]), ctx.msm_wait(jobs[1])
+    assert np.array_equal(r0, want)
+    sc = np.zeros((n, 4), np.uint64)
+    d.download(sc)
+    assert np.array_equal(r1, O.msm_g1(b.export()[:n - 1000], sc[:n - 1000]))

@@ -51,10 +51,16 @@ SIGNATURES = [
     ("zkmi_bases_create_g2", ctypes.c_int, [vp, u64p, sz, ctypes.POINTER(vp)]),
     ("zkmi_bases_destroy", None, [vp]),
     ("zkmi_bases_len", sz, [vp]),
+    ("zkmi_bases_export", ctypes.c_int, [vp, u64p]),
+    ("zkmi_bases_generate_g1", ctypes.c_int, [vp, ctypes.c_uint64, sz, ctypes.POINTER(vp)]),
+    ("zkmi_bases_generate_g2", ctypes.c_int, [vp, ctypes.c_uint64, sz, ctypes.POINTER(vp)]),
+    ("zkmi_scalars_generate", ctypes.c_int, [vp, ctypes.c_uint64, sz, vp]),
     ("zkmi_msm_g1", ctypes.c_int, [vp, vp, sz, u64p, sz, u64p]),
     ("zkmi_msm_g2", ctypes.c_int, [vp, vp, sz, u64p, sz, u64p]),
     ("zkmi_msm_g1_device", ctypes.c_int, [vp, vp, sz, vp, sz, u64p]),
     ("zkmi_msm_g2_device", ctypes.c_int, [vp, vp, sz, vp, sz, u64p]),
+    ("zkmi_msm_submit", ctypes.c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp)]),
+    ("zkmi_msm_wait", ctypes.c_int, [vp, u64p]),
     ("zkmi_msm_set_window", ctypes.c_int, [vp, ctypes.c_int]),
     ("zkmi_g1_add", ctypes.c_int, [u64p, u64p, u64p]),
     ("zkmi_g2_add", ctypes.c_int, [u64p, u64p, u64p]),

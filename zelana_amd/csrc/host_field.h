@@ -49,33 +49,35 @@ inline uint64_t add4(uint64_t o[4], const uint64_t a[4], const uint64_t b[4]) {
   }
   return c;
 }
+// Fully unrolled CIOS; q < 2^254 leaves the top word's 2 high bits free, so
+// the running value never exceeds 5 words ("no-carry" Montgomery).
+#define ZKH_MAC(t, a, b, c)                 \
+  do {                                      \
+    u128 x_ = (u128)(a) * (b) + (t) + (c);  \
+    (t) = (uint64_t)x_;                     \
+    (c) = (uint64_t)(x_ >> 64);             \
+  } while (0)
 inline F4 fmul(const F4& a, const F4& b) {
-  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
-  for (int i = 0; i < 4; i++) {
-    uint64_t c = 0;
-    for (int j = 0; j < 4; j++) {
-      u128 x = (u128)a.l[j] * b.l[i] + t[j] + c;
-      t[j] = (uint64_t)x;
-      c = (uint64_t)(x >> 64);
-    }
-    u128 s = (u128)t[4] + c;
-    t[4] = (uint64_t)s;
-    t[5] = (uint64_t)(s >> 64);
-    uint64_t m = t[0] * QINV;
-    u128 x = (u128)m * QP[0] + t[0];
-    c = (uint64_t)(x >> 64);
-    for (int j = 1; j < 4; j++) {
-      x = (u128)m * QP[j] + t[j] + c;
-      t[j - 1] = (uint64_t)x;
-      c = (uint64_t)(x >> 64);
-    }
-    s = (u128)t[4] + c;
-    t[3] = (uint64_t)s;
-    t[4] = t[5] + (uint64_t)(s >> 64);
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, c, m, hi;
+#define ZKH_ROUND(bi)                                                     \
+  c = 0;                                                                  \
+  ZKH_MAC(t0, a.l[0], bi, c);                                             \
+  ZKH_MAC(t1, a.l[1], bi, c);                                             \
+  ZKH_MAC(t2, a.l[2], bi, c);                                             \
+  ZKH_MAC(t3, a.l[3], bi, c);                                             \
+  hi = c;                                                                 \
+  m = t0 * QINV;                                                          \
+  c = (uint64_t)(((u128)m * QP[0] + t0) >> 64);                           \
+  {                                                                       \
+    u128 x_ = (u128)m * QP[1] + t1 + c; t0 = (uint64_t)x_; c = (uint64_t)(x_ >> 64); \
+    x_ = (u128)m * QP[2] + t2 + c; t1 = (uint64_t)x_; c = (uint64_t)(x_ >> 64);      \
+    x_ = (u128)m * QP[3] + t3 + c; t2 = (uint64_t)x_; c = (uint64_t)(x_ >> 64);      \
+    t3 = hi + c;                                                          \
   }
-  F4 r;
-  if (t[4] || geq(t, QP)) sub4(t, t, QP);
-  memcpy(r.l, t, 32);
+  ZKH_ROUND(b.l[0]) ZKH_ROUND(b.l[1]) ZKH_ROUND(b.l[2]) ZKH_ROUND(b.l[3])
+#undef ZKH_ROUND
+  F4 r = {{t0, t1, t2, t3}};
+  if (geq(r.l, QP)) sub4(r.l, r.l, QP);
   return r;
 }
 inline F4 fadd(const F4& a, const F4& b) {

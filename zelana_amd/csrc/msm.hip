@@ -3,12 +3,13 @@
 // a7/a8), called by ark-groth16 for h/l/a/b_g1 (G1) and b_g2 (G2).
 //
 // Pipeline (one HIP stream, all intermediate data resident in HBM):
-//   1. k_msm_hist     signed c-bit digits of every scalar (recomputed on the
-//                     fly, never stored), one atomic per non-zero digit into a
-//                     per-(window,bucket) histogram.  Bases at infinity skipped.
-//   2. scan           exclusive prefix sum -> bucket offsets (counting sort).
-//   3. k_msm_scatter  digits again; each (window,bucket,point,sign) lands at
-//                     its sorted slot.  Order inside a bucket is irrelevant:
+//   1. k_sort_count   two-level counting sort, pass 1: workgroup (chunk of 64K
+//                     points, window) recomputes the signed c-bit digits and
+//                     counts them in an LDS histogram (packed u16, no global
+//                     atomics).  Bases at infinity are skipped.
+//   2. prefix/scan    per-(window,bucket) chunk prefixes + global bucket starts.
+//   3. k_sort_scatter pass 2: LDS atomic rank -> each (point, sign) lands in its
+//                     bucket's slot.  Order inside a bucket is irrelevant:
 //                     group addition is exact, so results are bit-identical.
 //   4. k_msm_acc0     load balance by construction: every thread owns a fixed
 //                     chunk of L sorted entries (not a bucket), accumulating
@@ -29,6 +30,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 
 #include "ec.h"
 #include "zkmi_internal.h"
@@ -134,46 +136,84 @@ __device__ __forceinline__ void scalar_digits(const uint32_t* __restrict__ scala
   }
 }
 
+// Signed digits of every scalar, once per MSM: digits[w * n + i] (int32,
+// 0 = nothing to add; bases at infinity get all-zero digits).
 template <int C>
-__global__ void __launch_bounds__(256) k_msm_hist(const uint32_t* __restrict__ scalars,
-                                                  const uint32_t* __restrict__ bases, int pw, size_t n,
-                                                  uint32_t* __restrict__ counts) {
+__global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars,
+                                                    const uint32_t* __restrict__ bases, int pw, size_t n,
+                                                    int32_t* __restrict__ digits) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (bases[i * pw + pw - 1] >> 31) return;  // base at infinity contributes nothing
   constexpr int W = msm_windows(C);
-  constexpr uint32_t B = 1u << (C - 1);
   int32_t d[W];
   scalar_digits<C>(scalars, i, d);
+  const bool inf = bases[i * pw + pw - 1] >> 31;
 #pragma unroll
-  for (int w = 0; w < W; w++) {
-    if (d[w] != 0) {
-      uint32_t idx = (uint32_t)(d[w] < 0 ? -d[w] : d[w]) - 1;
-      atomicAdd(&counts[w * B + idx], 1u);
-    }
-  }
+  for (int w = 0; w < W; w++) digits[(size_t)w * n + i] = inf ? 0 : d[w];
 }
 
-template <int C>
-__global__ void __launch_bounds__(256) k_msm_scatter(const uint32_t* __restrict__ scalars,
-                                                     const uint32_t* __restrict__ bases, int pw, size_t n,
-                                                     uint32_t* __restrict__ cursor, uint32_t* __restrict__ sval,
-                                                     uint32_t* __restrict__ skey) {
-  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (bases[i * pw + pw - 1] >> 31) return;
-  constexpr int W = msm_windows(C);
-  constexpr uint32_t B = 1u << (C - 1);
-  int32_t d[W];
-  scalar_digits<C>(scalars, i, d);
-#pragma unroll
-  for (int w = 0; w < W; w++) {
-    if (d[w] != 0) {
-      uint32_t idx = (uint32_t)(d[w] < 0 ? -d[w] : d[w]) - 1;
-      uint32_t key = w * B + idx;
-      uint32_t pos = atomicAdd(&cursor[key], 1u);
-      sval[pos] = (uint32_t)i | (d[w] < 0 ? 0x80000000u : 0u);
-      skey[pos] = key;
+// Two-level counting sort.  Workgroup (chunk, w) owns up to SORT_CH points of
+// window w and counts its digits in an LDS histogram of packed u16 counters
+// (2^(c-1) buckets -> 64 KB at c = 16, 128 KB at c = 17): no global atomics.
+constexpr uint32_t SORT_CH = 65535;  // < 2^16 so a u16 counter cannot overflow
+constexpr int SORT_THREADS = 1024;
+
+__global__ void __launch_bounds__(SORT_THREADS) k_sort_count(const int32_t* __restrict__ digits, size_t n, uint32_t B,
+                                                             uint32_t nchunk, uint32_t* __restrict__ counts) {
+  extern __shared__ uint32_t hist[];  // B/2 words of two u16 counters
+  const uint32_t chunk = blockIdx.x, w = blockIdx.y;
+  for (uint32_t k = threadIdx.x; k < B / 2; k += SORT_THREADS) hist[k] = 0;
+  __syncthreads();
+  const int32_t* dg = digits + (size_t)w * n;
+  size_t lo = (size_t)chunk * SORT_CH, hi = lo + SORT_CH < n ? lo + SORT_CH : n;
+  for (size_t i = lo + threadIdx.x; i < hi; i += SORT_THREADS) {
+    int32_t d = dg[i];
+    if (d != 0) {
+      uint32_t idx = (uint32_t)(d < 0 ? -d : d) - 1;
+      atomicAdd(&hist[idx >> 1], 1u << ((idx & 1) * 16));
+    }
+  }
+  __syncthreads();
+  uint32_t* out = counts + ((size_t)w * nchunk + chunk) * B;
+  for (uint32_t b = threadIdx.x; b < B; b += SORT_THREADS) out[b] = (hist[b >> 1] >> ((b & 1) * 16)) & 0xFFFFu;
+}
+
+// per (w, b): counts[w][c][b] -> exclusive prefix over c (in place); totals[w*B+b]
+__global__ void __launch_bounds__(256) k_sort_chunk_prefix(uint32_t* __restrict__ counts, uint32_t nchunk, uint32_t B,
+                                                           uint32_t K, uint32_t* __restrict__ totals) {
+  uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  uint32_t w = k / B, b = k % B;
+  uint32_t run = 0;
+  for (uint32_t c = 0; c < nchunk; c++) {
+    uint32_t* p = counts + ((size_t)w * nchunk + c) * B + b;
+    uint32_t v = *p;
+    *p = run;
+    run += v;
+  }
+  totals[k] = run;
+}
+
+__global__ void __launch_bounds__(SORT_THREADS) k_sort_scatter(const int32_t* __restrict__ digits, size_t n, uint32_t B,
+                                                               uint32_t nchunk, const uint32_t* __restrict__ cprefix,
+                                                               const uint32_t* __restrict__ bstart,
+                                                               uint32_t* __restrict__ sval) {
+  extern __shared__ uint32_t hist[];
+  const uint32_t chunk = blockIdx.x, w = blockIdx.y;
+  for (uint32_t k = threadIdx.x; k < B / 2; k += SORT_THREADS) hist[k] = 0;
+  __syncthreads();
+  const uint32_t* cp = cprefix + ((size_t)w * nchunk + chunk) * B;
+  const uint32_t* bs = bstart + (size_t)w * B;
+  const int32_t* dg = digits + (size_t)w * n;
+  size_t lo = (size_t)chunk * SORT_CH, hi = lo + SORT_CH < n ? lo + SORT_CH : n;
+  for (size_t i = lo + threadIdx.x; i < hi; i += SORT_THREADS) {
+    int32_t d = dg[i];
+    if (d != 0) {
+      uint32_t idx = (uint32_t)(d < 0 ? -d : d) - 1;
+      uint32_t sh = (idx & 1) * 16;
+      uint32_t old = atomicAdd(&hist[idx >> 1], 1u << sh);
+      uint32_t rank = (old >> sh) & 0xFFFFu;
+      sval[bs[idx] + cp[idx] + rank] = (uint32_t)i | (d < 0 ? 0x80000000u : 0u);
     }
   }
 }
@@ -234,7 +274,7 @@ __global__ void __launch_bounds__(256) k_scan_add(uint32_t* __restrict__ out, ui
   if (i >= K) return;
   uint32_t v = out[i] + bs[i / 1024];
   out[i] = v;
-  cursor[i] = v;
+  if (cursor) cursor[i] = v;
 }
 
 // ------------------------------------------------------- bucket accumulation
@@ -244,28 +284,53 @@ __global__ void __launch_bounds__(256) k_scan_add(uint32_t* __restrict__ out, ui
 // stays sorted; a run made only of invalid slots is never written.
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
 
+// bucket containing sorted position p: largest k with bstart[k] <= p < bstart[k+1]
+__device__ __forceinline__ uint32_t bucket_of(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t p) {
+  uint32_t lo = 0, hi = K;  // invariant: bstart[lo] <= p < bstart[hi]
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (bstart[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
 template <class G>
-__global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ skey,
-                                                  uint32_t M, uint32_t L, uint32_t nchunks,
+__global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bstart,
+                                                  uint32_t K, uint32_t L, uint32_t nchunks,
                                                   const uint32_t* __restrict__ bases, uint32_t* __restrict__ buckets,
                                                   uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                                                  uint32_t* __restrict__ xpts) {
+                                                  uint32_t* __restrict__ xpts, uint32_t* __restrict__ open_flag) {
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nchunks) return;
-  uint32_t start = t * L, end = min(start + L, M);
-  uint32_t kprev = start > 0 ? skey[start - 1] : NOKEY;
-  uint32_t knext = end < M ? skey[end] : NOKEY;
-  uint32_t first_key = skey[start], last_key = skey[end - 1];
+  const uint32_t M = bstart[K];
+  uint32_t start = t * L;
+  if (start >= M) {
+    // beyond the data: keep the partial list sorted with max-key placeholders
+    xkey[2 * t + 1] = K;
+    xvalid[2 * t + 1] = 0;
+    xkey[2 * t + 2] = K;
+    xvalid[2 * t + 2] = 0;
+    if (t == 0) {
+      xkey[0] = K;
+      xvalid[0] = 0;
+    }
+    return;
+  }
+  uint32_t end = min(start + L, M);
+  uint32_t cur = bucket_of(bstart, K, start);
+  const uint32_t first_key = cur;
+  uint32_t next_b = bstart[cur + 1];
+  const bool left_cut = bstart[cur] < start;
   bool head_done = false, tail_done = false;
   Xyzz<F> acc = xyzz_inf<F>();
-  uint32_t cur = first_key;
   bool first_run = true;
   for (uint32_t p = start; p < end; p++) {
-    uint32_t k = skey[p];
-    if (k != cur) {
-      if (first_run && cur == kprev) {
+    if (p == next_b) {
+      // run of `cur` ends here (complete on the right)
+      if (first_run && left_cut) {
         xkey[2 * t + 1] = cur;
         xvalid[2 * t + 1] = 1;
         st_xyzz<G>(xpts + (size_t)(2 * t + 1) * XW, acc);
@@ -274,16 +339,19 @@ __global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ s
         st_xyzz<G>(buckets + (size_t)cur * XW, acc);
       }
       acc = xyzz_inf<F>();
-      cur = k;
       first_run = false;
+      do {
+        cur++;
+        next_b = bstart[cur + 1];
+      } while (next_b == p);  // skip empty buckets
     }
     uint32_t v = sval[p];
     Aff<F> P = ld_aff<G>(bases, v & 0x7FFFFFFFu);
     if (v >> 31) P.y = F::neg(P.y);
     acc = xyzz_madd(acc, P);
   }
-  bool left_open = first_run && cur == kprev;
-  bool right_open = cur == knext;
+  bool left_open = first_run && left_cut;
+  bool right_open = next_b > end;
   if (left_open) {
     xkey[2 * t + 1] = cur;
     xvalid[2 * t + 1] = 1;
@@ -297,12 +365,13 @@ __global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ s
   } else {
     st_xyzz<G>(buckets + (size_t)cur * XW, acc);
   }
+  if (left_open || right_open) atomicOr(open_flag, 1u);
   if (!head_done) {
     xkey[2 * t + 1] = first_key;
     xvalid[2 * t + 1] = 0;
   }
   if (!tail_done) {
-    xkey[2 * t + 2] = last_key;
+    xkey[2 * t + 2] = cur;
     xvalid[2 * t + 2] = 0;
   }
   if (t == 0) {
@@ -316,11 +385,12 @@ __global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ x
                                                   const uint32_t* __restrict__ xpts, uint32_t M, uint32_t L,
                                                   uint32_t nchunks, uint32_t* __restrict__ buckets,
                                                   uint32_t* __restrict__ ykey, uint32_t* __restrict__ yvalid,
-                                                  uint32_t* __restrict__ ypts, uint32_t* __restrict__ any_open) {
+                                                  uint32_t* __restrict__ ypts, const uint32_t* __restrict__ prev_open,
+                                                  uint32_t* __restrict__ any_open) {
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nchunks) return;
+  if (t >= nchunks || *prev_open == 0) return;
   uint32_t start = t * L, end = min(start + L, M);
   uint32_t kprev = start > 0 ? xkey[start - 1] : NOKEY;
   uint32_t knext = end < M ? xkey[end] : NOKEY;
@@ -384,83 +454,106 @@ __global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ x
 }
 
 // --------------------------------------------------------- bucket reduction
-// LDS tree over n (power of two) threads; sh holds n/2 points.  Result valid
-// in thread 0.
-template <class F, int N>
-__device__ __forceinline__ Xyzz<F> block_tree_sum(Xyzz<F> v, Xyzz<F>* sh) {
-  int t = threadIdx.x;
-  for (int s = N >> 1; s > 0; s >>= 1) {
-    if (t >= s && t < 2 * s) sh[t - s] = v;
-    __syncthreads();
-    if (t < s) v = xyzz_add(v, sh[t]);
-    __syncthreads();
-  }
-  return v;
-}
 
-// Generic tree sum over `cnt` <= 256 XYZZ terms with 256 threads (LDS tree).  Term t of block
-// (x, w) lives at element index  base(x, w) + map(t):
-//   mode 0 (rows): C[w][h=x] = sum_{l < 2^lb} B[w][(h << lb) + l]
-//   mode 1 (cols): D[w][l=x] = sum_{h < 2^hb} B[w][(h << lb) + l]
-//   mode 2 (bits): x = j;  j < lb:  U_j = sum_{l: bit j} D[w][l]
-//                          j < bb:  U_j = sum_{h: bit j-lb} C[w][h]
-//                          j == bb: T   = sum_h C[w][h]      (canonical output)
+// Bucket reduction jobs, one per wave (4 per 256-thread workgroup) so that a
+// 256-term sum occupies 64 lanes, not 256: every lane folds up to 4 terms,
+// then a 6-level LDS tree.  One xyzz_add call site in a uniform loop (a second
+// inlined copy doubles VGPRs and spills).
+//   FUSED (rows + cols):  job < W*2^hb :  C[w][h] = sum_{l < 2^lb} B[w][(h << lb) + l]
+//                         else         :  D[w][l] = sum_{h < 2^hb} B[w][(h << lb) + l]
+//   BITS:  job = w*(bb+1) + j:  j < lb : U_j = sum_{l: bit j} D[w][l]
+//                               j < bb : U_j = sum_{h: bit j-lb} C[w][h]
+//                               j = bb : T   = sum_h C[w][h]      (canonical output)
+// Empty buckets were never written (no memset): bstart says which are live.
 __device__ __forceinline__ uint32_t insert_bit(uint32_t t, int bit) {
   return (((t >> bit) << (bit + 1)) | (1u << bit) | (t & ((1u << bit) - 1)));
 }
-template <class G, int MODE>
+template <class G, bool BITS>
 __global__ void __launch_bounds__(256) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
-                                                int lb, int hb, uint32_t* __restrict__ out) {
+                                                const uint32_t* __restrict__ bstart, int lb, int hb, int W,
+                                                uint32_t* __restrict__ out0, uint32_t* __restrict__ out1) {
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
-  __shared__ Xyzz<F> sh[128];
+  __shared__ Xyzz<F> sh[4][32];
   const int bb = lb + hb;
-  const uint32_t x = blockIdx.x, w = blockIdx.y;
-  const uint32_t* src;
-  uint32_t cnt;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t job = blockIdx.x * 4 + wave;
+  const uint32_t njobs = BITS ? (uint32_t)W * (bb + 1) : (uint32_t)W * ((1u << hb) + (1u << lb));
+  const bool live = job < njobs;
+  const uint32_t* src = src0;
+  uint32_t cnt = 0, stride = 1, bucket0 = 0;
   int bit = -1;
-  if (MODE == 0) {
-    src = src0 + (((size_t)w << bb) + ((size_t)x << lb)) * XW;
-    cnt = 1u << lb;
-  } else if (MODE == 1) {
-    src = src0 + (((size_t)w << bb) + x) * XW;
-    cnt = 1u << hb;
-  } else {
-    if ((int)x < lb) {
-      src = src1 + ((size_t)w << lb) * XW;  // D
-      cnt = 1u << (lb - 1);
-      bit = (int)x;
-    } else if ((int)x < bb) {
-      src = src0 + ((size_t)w << hb) * XW;  // C
-      cnt = 1u << (hb - 1);
-      bit = (int)x - lb;
+  uint32_t* dst = nullptr;
+  bool canon = false;
+  if (live) {
+    if (!BITS) {
+      uint32_t nrow = (uint32_t)W << hb;
+      if (job < nrow) {  // row h of window w
+        uint32_t w = job >> hb, h = job & ((1u << hb) - 1);
+        bucket0 = (w << bb) + (h << lb);
+        cnt = 1u << lb;
+        stride = 1;
+        dst = out0 + (size_t)job * XW;
+      } else {  // column l of window w
+        uint32_t jj = job - nrow, w = jj >> lb, l = jj & ((1u << lb) - 1);
+        bucket0 = (w << bb) + l;
+        cnt = 1u << hb;
+        stride = 1u << lb;
+        dst = out1 + (size_t)jj * XW;
+      }
+      src = src0 + (size_t)bucket0 * XW;
     } else {
-      src = src0 + ((size_t)w << hb) * XW;
-      cnt = 1u << hb;
+      uint32_t w = job / (bb + 1), j = job % (bb + 1);
+      if ((int)j < lb) {
+        src = src1 + ((size_t)w << lb) * XW;
+        cnt = 1u << (lb - 1);
+        bit = (int)j;
+      } else if ((int)j < bb) {
+        src = src0 + ((size_t)w << hb) * XW;
+        cnt = 1u << (hb - 1);
+        bit = (int)j - lb;
+      } else {
+        src = src0 + ((size_t)w << hb) * XW;
+        cnt = 1u << hb;
+      }
+      dst = out0 + (size_t)job * XW;
+      canon = true;
     }
   }
-  // cnt <= 256 (windows <= 17 bits): one term per thread.  A second inlined
-  // addition call site here would double the kernel's VGPRs and spill.
   Xyzz<F> v = xyzz_inf<F>();
-  const uint32_t t = threadIdx.x;
-  if (t < cnt) {
-    uint32_t e;
-    if (MODE == 0) e = t;
-    else if (MODE == 1) e = t << lb;
-    else e = bit < 0 ? t : insert_bit(t, bit);
-    v = ld_xyzz<G>(src + (size_t)e * XW);
+  for (int step = 0; step < 4 + 6; step++) {
+    Xyzz<F> q;
+    bool act = false;
+    if (step < 4) {
+      uint32_t t = lane + 64u * step;
+      if (live && t < cnt) {
+        uint32_t e = BITS ? (bit < 0 ? t : insert_bit(t, bit)) : t * stride;
+        bool nonempty = BITS ? true : bstart[bucket0 + e + 1] > bstart[bucket0 + e];
+        if (nonempty) {
+          q = ld_xyzz<G>(src + (size_t)e * XW);
+          act = true;
+        }
+      }
+    } else {
+      uint32_t sz = 32u >> (step - 4);
+      if (lane >= sz && lane < 2 * sz) sh[wave][lane - sz] = v;
+      __syncthreads();
+      if (lane < sz) {
+        q = sh[wave][lane];
+        act = true;
+      }
+    }
+    if (act) v = xyzz_is_inf(v) ? q : xyzz_add(v, q);
+    if (step >= 4) __syncthreads();
   }
-  v = block_tree_sum<F, 256>(v, sh);
-  if (threadIdx.x == 0) {
-    if (MODE == 2) {
+  if (live && lane == 0) {
+    if (canon) {
       v.x = Io<F>::canon(v.x);
       v.y = Io<F>::canon(v.y);
       v.zz = Io<F>::canon(v.zz);
       v.zzz = Io<F>::canon(v.zzz);
-      st_xyzz<G>(out + ((size_t)w * (bb + 1) + x) * XW, v);
-    } else {
-      st_xyzz<G>(out + ((size_t)w * gridDim.x + x) * XW, v);
     }
+    st_xyzz<G>(dst, v);
   }
 }
 
@@ -505,6 +598,154 @@ __global__ void __launch_bounds__(256) k_bases_convert(const uint32_t* __restric
     st_fe(q + 16, reduce<FqP>(y.c0));
     st_fe(q + 24, reduce<FqP>(y.c1));
   }
+}
+
+// ------------------------------------------------ synthetic inputs (bench)
+// Deterministic pseudo-random inputs generated where they will live (HBM):
+//   scalars: splitmix64 stream per index, 254-bit candidates rejected until < r
+//   bases:   P_i = k_i * G with k_i from the same stream (253-bit), G the
+//            standard generator (G1: (1, 2); G2: the arkworks/EIP-197 one),
+//            normalised to affine (internal Montgomery form)
+__device__ __forceinline__ uint64_t splitmix64(uint64_t& x) {
+  uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__constant__ uint64_t FR_MOD64[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
+                                     0x30644e72e131a029ull};
+__global__ void __launch_bounds__(256) k_gen_scalars(uint64_t seed, size_t n, uint64_t* __restrict__ out) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t st = seed * 0x100000001B3ull ^ (i * 0x9E3779B97F4A7C15ull);
+  uint64_t v[4];
+  for (;;) {
+    for (int k = 0; k < 4; k++) v[k] = splitmix64(st);
+    v[3] &= 0x3FFFFFFFFFFFFFFFull;  // 254 bits
+    bool lt = false;
+    for (int k = 3; k >= 0; k--) {
+      if (v[k] != FR_MOD64[k]) {
+        lt = v[k] < FR_MOD64[k];
+        break;
+      }
+    }
+    if (lt) break;
+  }
+  for (int k = 0; k < 4; k++) out[i * 4 + k] = v[k];
+}
+// G2 generator (canonical): x = (x0, x1), y = (y0, y1)
+__constant__ uint32_t G2GEN[32] = {
+    0xd992f6edu, 0x46debd5cu, 0xf75edaddu, 0x674322d4u, 0x5e5c4479u, 0x426a0066u, 0x121f1e76u, 0x1800deefu,
+    0xaef312c2u, 0x97e485b7u, 0x35a9e712u, 0xf1aa4933u, 0x31fb5d25u, 0x7260bfb7u, 0x920d483au, 0x198e9393u,
+    0x66fa7daau, 0x4ce6cc01u, 0x0c43d37bu, 0xe3d1e769u, 0x8dcb408fu, 0x4aab7180u, 0xdb8c6debu, 0x12c85ea5u,
+    0xd122975bu, 0x55acdadcu, 0x70b38ef3u, 0xbc4b3133u, 0x690c3395u, 0xec9e99adu, 0x585ff075u, 0x090689d0u};
+
+__device__ Fe fq_inv(const Fe& a) {
+  const uint64_t e[4] = {0x3c208c16d87cfd45ull, 0x97816a916871ca8dull, 0xb85045b68181585dull, 0x30644e72e131a029ull};
+  return pow<FqP>(a, e);  // a^(q-2)
+}
+template <class G>
+__global__ void __launch_bounds__(256) k_gen_bases(uint64_t seed, size_t n, uint32_t* __restrict__ out) {
+  using F = typename G::F;
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t st = (seed + 0x51ED270Bull) * 0x100000001B3ull ^ (i * 0xD1B54A32D192ED03ull);
+  uint64_t k[4];
+  for (int j = 0; j < 4; j++) k[j] = splitmix64(st);
+  k[3] &= 0x1FFFFFFFFFFFFFFFull;  // 253 bits < r
+  k[0] |= 1;                       // never zero
+  Aff<F> g;
+  if constexpr (G::CW == 8) {
+    g.x = to_mont<FqP>(Fe{{1, 0, 0, 0, 0, 0, 0, 0, 0}});
+    g.y = to_mont<FqP>(Fe{{2, 0, 0, 0, 0, 0, 0, 0, 0}});
+  } else {
+    g.x = {to_mont<FqP>(ld_fe(G2GEN)), to_mont<FqP>(ld_fe(G2GEN + 8))};
+    g.y = {to_mont<FqP>(ld_fe(G2GEN + 16)), to_mont<FqP>(ld_fe(G2GEN + 24))};
+  }
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (int b = 252; b >= 0; b--) {
+    acc = xyzz_dbl(acc);
+    if ((k[b >> 6] >> (b & 63)) & 1) acc = xyzz_madd(acc, g);
+  }
+  uint32_t* q = out + i * G::PW;
+  if constexpr (G::CW == 8) {
+    Fe izz = fq_inv(acc.zz), izzz = fq_inv(acc.zzz);
+    st_fe(q, reduce<FqP>(mul<FqP>(acc.x, izz)));
+    st_fe(q + 8, reduce<FqP>(mul<FqP>(acc.y, izzz)));
+  } else {
+    // Fq2 inverse via the norm
+    auto inv2 = [](const Fe2& a) {
+      Fe nrm = add<FqP>(sqr<FqP>(a.c0), sqr<FqP>(a.c1));
+      Fe ni = fq_inv(nrm);
+      return Fe2{mul<FqP>(a.c0, ni), neg<FqP>(mul<FqP>(a.c1, ni))};
+    };
+    Fe2 x = f2_mul(acc.x, inv2(acc.zz)), y = f2_mul(acc.y, inv2(acc.zzz));
+    st_fe(q, reduce<FqP>(x.c0));
+    st_fe(q + 8, reduce<FqP>(x.c1));
+    st_fe(q + 16, reduce<FqP>(y.c0));
+    st_fe(q + 24, reduce<FqP>(y.c1));
+  }
+}
+// internal -> canonical affine (export for checking)
+template <class G>
+__global__ void __launch_bounds__(256) k_bases_export(const uint32_t* __restrict__ in, size_t n,
+                                                      uint32_t* __restrict__ out) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* p = in + i * G::PW;
+  uint32_t* q = out + i * G::PW;
+  if (p[G::PW - 1] >> 31) {
+    for (int k = 0; k < G::PW; k++) q[k] = 0;
+    return;
+  }
+  for (int c = 0; c < G::PW / 8; c++) st_fe(q + 8 * c, from_mont<FqP>(ld_fe(p + 8 * c)));
+}
+
+int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t n, zkmi_bases** out) {
+  int pw = g2 ? 32 : 16;
+  uint32_t* d_pts = nullptr;
+  if (hipMalloc(&d_pts, std::max<size_t>(1, n) * pw * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("hipMalloc(%zu) failed for bases", n * pw * 4);
+    return ZKMI_ENOMEM;
+  }
+  if (n) {
+    unsigned grid = (unsigned)((n + 255) / 256);
+    if (g2) k_gen_bases<G2T><<<grid, 256, 0, ctx->stream>>>(seed, n, d_pts);
+    else k_gen_bases<G1T><<<grid, 256, 0, ctx->stream>>>(seed, n, d_pts);
+    ZK_HIP(hipGetLastError());
+  }
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  zkmi_bases* b = new zkmi_bases;
+  b->ctx = ctx;
+  b->g2 = g2;
+  b->n = n;
+  b->d_pts = d_pts;
+  *out = b;
+  return 0;
+}
+int bases_export(const zkmi_bases* b, uint64_t* host_out) {
+  zkmi_ctx* ctx = b->ctx;
+  int pw = b->g2 ? 32 : 16;
+  uint32_t* tmp;
+  ZK_TRY(ctx->ws.get("bases_export", std::max<size_t>(1, b->n) * pw * 4, (void**)&tmp));
+  if (b->n) {
+    unsigned grid = (unsigned)((b->n + 255) / 256);
+    if (b->g2) k_bases_export<G2T><<<grid, 256, 0, ctx->stream>>>(b->d_pts, b->n, tmp);
+    else k_bases_export<G1T><<<grid, 256, 0, ctx->stream>>>(b->d_pts, b->n, tmp);
+    ZK_HIP(hipGetLastError());
+    ZK_HIP(hipMemcpyAsync(host_out, tmp, b->n * pw * 4, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+int scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_out) {
+  if (n) {
+    k_gen_scalars<<<(unsigned)((n + 255) / 256), 256, 0, ctx->stream>>>(seed, n, (uint64_t*)d_out);
+    ZK_HIP(hipGetLastError());
+  }
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  return 0;
 }
 
 int bases_from_device_canon(zkmi_ctx* ctx, int g2, const uint32_t* d_canon, size_t n, zkmi_bases** out) {
@@ -559,17 +800,14 @@ static int pick_window(size_t n) {
 }
 
 template <int C>
-static void launch_digits(bool scatter, hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw, size_t n,
-                          uint32_t* counts_or_cursor, uint32_t* sval, uint32_t* skey) {
-  unsigned grid = (unsigned)((n + 255) / 256);
-  if (!scatter) k_msm_hist<C><<<grid, 256, 0, st>>>(sc, bases, pw, n, counts_or_cursor);
-  else k_msm_scatter<C><<<grid, 256, 0, st>>>(sc, bases, pw, n, counts_or_cursor, sval, skey);
+static void launch_digits(hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw, size_t n, int32_t* dg) {
+  k_msm_digits<C><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(sc, bases, pw, n, dg);
 }
-static int dispatch_digits(int c, bool scatter, hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw,
-                           size_t n, uint32_t* cc, uint32_t* sval, uint32_t* skey) {
+static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw, size_t n,
+                           int32_t* dg) {
   switch (c) {
 #define ZK_C(CC) \
-  case CC: launch_digits<CC>(scatter, st, sc, bases, pw, n, cc, sval, skey); break;
+  case CC: launch_digits<CC>(st, sc, bases, pw, n, dg); break;
     ZK_C(4) ZK_C(5) ZK_C(6) ZK_C(7) ZK_C(8) ZK_C(9) ZK_C(10) ZK_C(11) ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15)
     ZK_C(16) ZK_C(17)
 #undef ZK_C
@@ -580,8 +818,25 @@ static int dispatch_digits(int c, bool scatter, hipStream_t st, const uint32_t* 
   return 0;
 }
 
+}  // namespace zk
+
+// An MSM in flight: GPU work and the D2H of the bit sums are queued on the
+// context stream; the host epilogue runs in zkmi_msm_wait, so a caller can
+// overlap it with the next MSM's kernels (submit k+1, then wait k).
+struct zkmi_msm_job {
+  zkmi_ctx* ctx;
+  int g2, c, W, bb;
+  uint32_t* host;  // pinned: W*(bb+1) canonical XYZZ
+  size_t host_words;
+  hipEvent_t done;
+  bool empty;
+};
+
+namespace zk {
+
 template <class G>
-static int msm_run(zkmi_ctx* ctx, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n, uint64_t* out) {
+static int msm_submit_t(zkmi_ctx* ctx, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n,
+                        zkmi_msm_job** out_job) {
   constexpr int XW = 4 * G::CW;
   hipStream_t st = ctx->stream;
   int c = ctx->msm_window > 0 ? ctx->msm_window : pick_window(n);
@@ -589,134 +844,167 @@ static int msm_run(zkmi_ctx* ctx, const uint32_t* d_bases, const uint32_t* d_sca
   uint32_t B = 1u << (c - 1);
   uint32_t K = (uint32_t)W * B;
   int bb = c - 1, lb = (bb + 1) / 2, hb = bb - lb;
-  if (n == 0 || n >= (1u << 31) || (size_t)W * n >= (1ull << 32)) {
-    if (n == 0) {
-      memset(out, 0, G::PW * 4);
-      return 0;
-    }
+  zkmi_msm_job* job = new zkmi_msm_job{ctx, G::CW == 16, c, W, bb, nullptr, 0, nullptr, n == 0};
+  *out_job = job;
+  if (n == 0) return 0;
+  if (n >= (1u << 31) || (size_t)W * n >= (1ull << 32)) {
     set_error("MSM size %zu too large for one call", n);
     return ZKMI_EINVAL;
   }
-  uint32_t *counts, *offs, *cursor, *bsums, *total, *sval, *skey, *buckets, *flag;
+  uint32_t nchunk = (uint32_t)((n + SORT_CH - 1) / SORT_CH);
+  uint32_t *counts, *bstart, *bsums, *sval, *buckets, *flags;
+  int32_t* digits;
   uint32_t nb = (K + 1023) / 1024;
   size_t Mmax = (size_t)W * n;
-  ZK_TRY(ctx->ws.get("msm_counts", (size_t)K * 4, (void**)&counts));
-  ZK_TRY(ctx->ws.get("msm_offs", (size_t)(K + 1) * 4, (void**)&offs));
-  ZK_TRY(ctx->ws.get("msm_cursor", (size_t)K * 4, (void**)&cursor));
+  ZK_TRY(ctx->ws.get("msm_digits", Mmax * 4, (void**)&digits));
+  ZK_TRY(ctx->ws.get("msm_counts", (size_t)K * nchunk * 4, (void**)&counts));
+  ZK_TRY(ctx->ws.get("msm_bstart", (size_t)(K + 1) * 4, (void**)&bstart));
   ZK_TRY(ctx->ws.get("msm_bsums", (size_t)nb * 4 + 16, (void**)&bsums));
-  ZK_TRY(ctx->ws.get("msm_total", 16, (void**)&total));
   ZK_TRY(ctx->ws.get("msm_sval", Mmax * 4, (void**)&sval));
-  ZK_TRY(ctx->ws.get("msm_skey", Mmax * 4, (void**)&skey));
   ZK_TRY(ctx->ws.get("msm_buckets", (size_t)K * XW * 4, (void**)&buckets));
-  ZK_TRY(ctx->ws.get("msm_flag", 16, (void**)&flag));
-
-  ZK_HIP(hipMemsetAsync(counts, 0, (size_t)K * 4, st));
-  ZK_HIP(hipMemsetAsync(buckets, 0, (size_t)K * XW * 4, st));
+  ZK_TRY(ctx->ws.get("msm_flags", 64 * 4, (void**)&flags));
+  ZK_HIP(hipMemsetAsync(flags, 0, 64 * 4, st));
   {
-    ScopedKernelTimer tm(ctx, "msm_hist");
-    ZK_TRY(dispatch_digits(c, false, st, d_scalars, d_bases, G::PW, n, counts, nullptr, nullptr));
+    ScopedKernelTimer tm(ctx, "msm_sort");
+    ZK_TRY(dispatch_digits(c, st, d_scalars, d_bases, G::PW, n, digits));
+    dim3 grid(nchunk, W);
+    size_t lds = (B / 2) * 4;
+    k_sort_count<<<grid, SORT_THREADS, lds, st>>>(digits, n, B, nchunk, counts);
+    k_sort_chunk_prefix<<<(K + 255) / 256, 256, 0, st>>>(counts, nchunk, B, K, bstart);
+    // exclusive scan of per-bucket totals (in bstart) -> bucket starts; bstart[K] = M
+    k_scan_blocks<<<nb, 256, 0, st>>>(bstart, K, bstart, bsums);
+    k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, bstart + K);
+    k_scan_add<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, bsums, nullptr);
+    k_sort_scatter<<<grid, SORT_THREADS, lds, st>>>(digits, n, B, nchunk, counts, bstart, sval);
+    ZK_HIP(hipGetLastError());
   }
+  // level 0: fixed-size chunks of the sorted list (sized from the upper bound
+  // W*n so no host round-trip is needed; chunks past M exit at once)
+  uint32_t L = (uint32_t)std::max<size_t>(4, (Mmax + (size_t)ctx->num_cus * 1024 - 1) / ((size_t)ctx->num_cus * 1024));
+  uint32_t nch = (uint32_t)((Mmax + L - 1) / L);
+  uint32_t *xkey, *xvalid, *xpts, *ykey, *yvalid, *ypts;
+  size_t xl = 2 * (size_t)nch + 1;
+  ZK_TRY(ctx->ws.get("msm_xkey", xl * 4 + 64, (void**)&xkey));
+  ZK_TRY(ctx->ws.get("msm_xvalid", xl * 4 + 64, (void**)&xvalid));
+  ZK_TRY(ctx->ws.get("msm_xpts", (xl + 2) * XW * 4, (void**)&xpts));
+  ZK_TRY(ctx->ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
+  ZK_TRY(ctx->ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
+  ZK_TRY(ctx->ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
   {
-    ScopedKernelTimer tm(ctx, "msm_scan");
-    k_scan_blocks<<<nb, 256, 0, st>>>(counts, K, offs, bsums);
-    k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, total);
-    k_scan_add<<<(K + 255) / 256, 256, 0, st>>>(offs, K, bsums, cursor);
+    ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2");
+    k_msm_acc0<G><<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, buckets, xkey, xvalid, xpts,
+                                                     &flags[0]);
+    ZK_HIP(hipGetLastError());
   }
-  uint32_t M = 0;
-  ZK_HIP(hipMemcpyAsync(&M, total, 4, hipMemcpyDeviceToHost, st));
+  // segmented reduction of cut runs: level 1 pairs (tail, head) halves,
+  // deeper levels only carry heavy buckets; each level exits on device when
+  // the previous one left nothing open (no host round-trips)
   {
-    ScopedKernelTimer tm(ctx, "msm_scatter");
-    ZK_TRY(dispatch_digits(c, true, st, d_scalars, d_bases, G::PW, n, cursor, sval, skey));
-  }
-  ZK_HIP(hipStreamSynchronize(st));
-  if (M > 0) {
-    // level 0: chunks sized for >= ~1024 threads per CU
-    uint32_t L = (uint32_t)std::max<size_t>(4, (M + (size_t)ctx->num_cus * 1024 - 1) / ((size_t)ctx->num_cus * 1024));
-    uint32_t nch = (M + L - 1) / L;
-    uint32_t *xkey, *xvalid, *xpts, *ykey, *yvalid, *ypts;
-    size_t xl = 2 * (size_t)nch + 1;
-    ZK_TRY(ctx->ws.get("msm_xkey", xl * 4, (void**)&xkey));
-    ZK_TRY(ctx->ws.get("msm_xvalid", xl * 4, (void**)&xvalid));
-    ZK_TRY(ctx->ws.get("msm_xpts", xl * XW * 4, (void**)&xpts));
-    ZK_TRY(ctx->ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
-    ZK_TRY(ctx->ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
-    ZK_TRY(ctx->ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
-    {
-      ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2");
-      k_msm_acc0<G><<<(nch + 255) / 256, 256, 0, st>>>(sval, skey, M, L, nch, d_bases, buckets, xkey, xvalid, xpts);
-      ZK_HIP(hipGetLastError());
-    }
-    // segmented reduction of cut runs
+    ScopedKernelTimer tm(ctx, "msm_accN");
     uint32_t cur_len = (uint32_t)xl;
-    int level = 1;
-    while (cur_len > 1) {
+    for (int level = 1; cur_len > 1; level++) {
+      if (level >= 63) {
+        set_error("msm: segmented reduction schedule too deep");
+        return ZKMI_EINVAL;
+      }
       uint32_t Ll = level == 1 ? 2 : 16;
       uint32_t nc = (cur_len + Ll - 1) / Ll;
-      ZK_HIP(hipMemsetAsync(flag, 0, 4, st));
-      {
-        ScopedKernelTimer tm(ctx, "msm_accN");
-        k_msm_accN<G><<<(nc + 255) / 256, 256, 0, st>>>(xkey, xvalid, xpts, cur_len, Ll, nc, buckets, ykey, yvalid,
-                                                        ypts, flag);
-        ZK_HIP(hipGetLastError());
-      }
-      uint32_t any = 0;
-      ZK_HIP(hipMemcpyAsync(&any, flag, 4, hipMemcpyDeviceToHost, st));
-      ZK_HIP(hipStreamSynchronize(st));
-      if (!any) break;
+      k_msm_accN<G><<<(nc + 255) / 256, 256, 0, st>>>(xkey, xvalid, xpts, cur_len, Ll, nc, buckets, ykey, yvalid,
+                                                      ypts, &flags[level - 1], &flags[level]);
       std::swap(xkey, ykey);
       std::swap(xvalid, yvalid);
       std::swap(xpts, ypts);
-      cur_len = 2 * nc + 1;
-      level++;
-      if (level > 64) {
-        set_error("msm: segmented reduction did not converge");
-        return ZKMI_EINVAL;
-      }
+      cur_len = nc == 1 ? 1 : 2 * nc + 1;
     }
+    ZK_HIP(hipGetLastError());
   }
-  // bucket reduction
+  // bucket reduction -> W*(bb+1) canonical bit sums
   uint32_t *Cb, *Db, *sums;
   ZK_TRY(ctx->ws.get("msm_C", (size_t)W * (1u << hb) * XW * 4, (void**)&Cb));
   ZK_TRY(ctx->ws.get("msm_D", (size_t)W * (1u << lb) * XW * 4, (void**)&Db));
   ZK_TRY(ctx->ws.get("msm_sums", (size_t)W * (bb + 1) * XW * 4, (void**)&sums));
   {
     ScopedKernelTimer tm(ctx, "msm_bucket_reduce");
-    k_msm_br<G, 0><<<dim3(1u << hb, W), 256, 0, st>>>(buckets, nullptr, lb, hb, Cb);
-    k_msm_br<G, 1><<<dim3(1u << lb, W), 256, 0, st>>>(buckets, nullptr, lb, hb, Db);
-    k_msm_br<G, 2><<<dim3(bb + 1, W), 256, 0, st>>>(Cb, Db, lb, hb, sums);
+    uint32_t jobs1 = (uint32_t)W * ((1u << hb) + (1u << lb)), jobs2 = (uint32_t)W * (bb + 1);
+    k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, st>>>(buckets, nullptr, bstart, lb, hb, W, Cb, Db);
+    k_msm_br<G, true><<<(jobs2 + 3) / 4, 256, 0, st>>>(Cb, Db, nullptr, lb, hb, W, sums, nullptr);
     ZK_HIP(hipGetLastError());
   }
-  std::vector<uint32_t> hs((size_t)W * (bb + 1) * XW);
-  ZK_HIP(hipMemcpyAsync(hs.data(), sums, hs.size() * 4, hipMemcpyDeviceToHost, st));
-  ZK_HIP(hipStreamSynchronize(st));
-  ZK_TRY(timer_flush(ctx));
-  // V_k over k < c*W: V_{c w + j} += U_{w,j}; V_{c w} += T_w
-  int nbits = c * W;
-  std::vector<uint32_t> V((size_t)nbits * XW, 0);
-  std::vector<uint32_t> Tw((size_t)W * XW);
-  for (int w = 0; w < W; w++) {
-    for (int j = 0; j < bb; j++)
-      memcpy(&V[((size_t)c * w + j) * XW], &hs[((size_t)w * (bb + 1) + j) * XW], XW * 4);
-  }
-  // T_w shares weight 2^{c w} with U_{w,0}: combine on the host side by
-  // passing it as an extra term (nbits + w slot) handled in the Horner helper.
-  std::vector<uint32_t> all((size_t)(nbits + W) * XW);
-  memcpy(all.data(), V.data(), V.size() * 4);
-  for (int w = 0; w < W; w++) memcpy(&all[((size_t)nbits + w) * XW], &hs[((size_t)w * (bb + 1) + bb) * XW], XW * 4);
-  if (G::CW == 8) msm_host_combine_g1(all.data(), nbits, W, c, out);
-  else msm_host_combine_g2(all.data(), nbits, W, c, out);
+  job->host_words = (size_t)W * (bb + 1) * XW;
+  ZK_TRY(ctx_pinned_get(ctx, job->host_words * 4, (void**)&job->host));
+  ZK_HIP(hipMemcpyAsync(job->host, sums, job->host_words * 4, hipMemcpyDeviceToHost, st));
+  ZK_HIP(hipEventCreateWithFlags(&job->done, hipEventDisableTiming));
+  ZK_HIP(hipEventRecord(job->done, st));
   return 0;
 }
 
-int msm_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
-               uint64_t* out_affine) {
+int msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+               zkmi_msm_job** job) {
+  *job = nullptr;
   if (!b || offset > b->n || n > b->n - offset) {
     set_error("msm: range [%zu, %zu) outside base set of %zu", offset, offset + n, b ? b->n : 0);
     return ZKMI_EINVAL;
   }
-  if (b->g2)
-    return msm_run<G2T>(ctx, b->d_pts + offset * 32, (const uint32_t*)d_scalars, n, out_affine);
-  return msm_run<G1T>(ctx, b->d_pts + offset * 16, (const uint32_t*)d_scalars, n, out_affine);
+  int rc = b->g2 ? msm_submit_t<G2T>(ctx, b->d_pts + offset * 32, (const uint32_t*)d_scalars, n, job)
+                 : msm_submit_t<G1T>(ctx, b->d_pts + offset * 16, (const uint32_t*)d_scalars, n, job);
+  if (rc != 0 && *job) {
+    msm_job_free(*job);
+    *job = nullptr;
+  }
+  return rc;
+}
+
+void msm_job_free(zkmi_msm_job* job) {
+  if (!job) return;
+  if (job->done) hipEventDestroy(job->done);
+  if (job->host) ctx_pinned_put(job->ctx, job->host);
+  delete job;
+}
+
+int msm_wait(zkmi_msm_job* job, uint64_t* out) {
+  if (!job) {
+    set_error("msm_wait: null job");
+    return ZKMI_EINVAL;
+  }
+  zkmi_ctx* ctx = job->ctx;
+  int PW = job->g2 ? 32 : 16, XW = 2 * PW;
+  if (job->empty) {
+    memset(out, 0, PW * 4);
+    msm_job_free(job);
+    return 0;
+  }
+  hipError_t e = hipEventSynchronize(job->done);
+  if (e != hipSuccess) {
+    set_error("msm_wait: %s", hipGetErrorString(e));
+    msm_job_free(job);
+    return ZKMI_EHIP;
+  }
+  int rc = timer_flush(ctx);
+  auto th0 = std::chrono::steady_clock::now();
+  // terms: V_{c w + j} = U_{w,j} (j < c-1), then T_w at weight 2^{c w}
+  int c = job->c, W = job->W, bb = job->bb, nbits = c * W;
+  std::vector<uint32_t> all((size_t)(nbits + W) * XW, 0);
+  for (int w = 0; w < W; w++) {
+    for (int j = 0; j < bb; j++)
+      memcpy(&all[((size_t)c * w + j) * XW], &job->host[((size_t)w * (bb + 1) + j) * XW], XW * 4);
+    memcpy(&all[((size_t)nbits + w) * XW], &job->host[((size_t)w * (bb + 1) + bb) * XW], XW * 4);
+  }
+  if (!job->g2) msm_host_combine_g1(all.data(), nbits, W, c, out);
+  else msm_host_combine_g2(all.data(), nbits, W, c, out);
+  if (ctx->timer.enabled) {
+    auto& t = ctx->timer.totals["msm_host_epilogue"];
+    t.first += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
+    t.second += 1;
+  }
+  msm_job_free(job);
+  return rc;
+}
+
+int msm_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+               uint64_t* out_affine) {
+  zkmi_msm_job* job;
+  ZK_TRY(msm_submit(ctx, b, offset, d_scalars, n, &job));
+  return msm_wait(job, out_affine);
 }
 
 }  // namespace zk

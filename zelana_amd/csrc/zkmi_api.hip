@@ -8,6 +8,16 @@
 
 namespace zk {
 
+// size of every pinned buffer handed out (pool bookkeeping)
+static std::map<void*, size_t>& ctx_pinned_sizes() {
+  static std::map<void*, size_t> m;
+  return m;
+}
+static size_t ctx_pinned_sizes_lookup(void* p, size_t dflt) {
+  auto it = ctx_pinned_sizes().find(p);
+  return it == ctx_pinned_sizes().end() ? dflt : it->second;
+}
+
 static thread_local char g_err[512] = "";
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -74,6 +84,31 @@ int timer_flush(zkmi_ctx* ctx) {
   return 0;
 }
 
+int ctx_pinned_get(zkmi_ctx* ctx, size_t bytes, void** out) {
+  for (size_t i = 0; i < ctx->pinned_free.size(); i++) {
+    if (ctx->pinned_free[i].second >= bytes) {
+      *out = ctx->pinned_free[i].first;
+      ctx->pinned_free.erase(ctx->pinned_free.begin() + i);
+      ctx_pinned_sizes()[*out] = ctx_pinned_sizes_lookup(*out, bytes);
+      return 0;
+    }
+  }
+  size_t sz = bytes < 4096 ? 4096 : bytes;
+  if (hipHostMalloc(out, sz, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("hipHostMalloc(%zu) failed", sz);
+    return ZKMI_ENOMEM;
+  }
+  ctx_pinned_sizes()[*out] = sz;
+  return 0;
+}
+void ctx_pinned_put(zkmi_ctx* ctx, void* p) {
+  auto& m = ctx_pinned_sizes();
+  auto it = m.find(p);
+  size_t sz = it == m.end() ? 0 : it->second;
+  ctx->pinned_free.push_back({p, sz});
+}
+
 }  // namespace zk
 
 using namespace zk;
@@ -122,6 +157,8 @@ void zkmi_ctx_destroy(zkmi_ctx* ctx) {
   hipStreamSynchronize(ctx->stream);
   timer_flush(ctx);
   ctx->ws.release_all();
+  for (auto& pb : ctx->pinned_free) hipHostFree(pb.first);
+  ctx->pinned_free.clear();
   hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -183,6 +220,22 @@ void zkmi_bases_destroy(zkmi_bases* b) {
   delete b;
 }
 size_t zkmi_bases_len(const zkmi_bases* b) { return b ? b->n : 0; }
+int zkmi_bases_export(const zkmi_bases* b, uint64_t* affine_out) {
+  if (!b) {
+    set_error("zkmi_bases_export: null bases");
+    return ZKMI_EINVAL;
+  }
+  return bases_export(b, affine_out);
+}
+int zkmi_bases_generate_g1(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** out) {
+  return bases_generate(ctx, 0, seed, n, out);
+}
+int zkmi_bases_generate_g2(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** out) {
+  return bases_generate(ctx, 1, seed, n, out);
+}
+int zkmi_scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_scalars) {
+  return scalars_generate(ctx, seed, n, d_scalars);
+}
 
 static int msm_host_scalars(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_t* scalars, size_t n,
                             uint64_t* out) {
@@ -223,6 +276,11 @@ int zkmi_msm_g2_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const 
   }
   return msm_device(ctx, b, offset, d_scalars, n, out_affine);
 }
+int zkmi_msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+                    zkmi_msm_job** job) {
+  return msm_submit(ctx, b, offset, d_scalars, n, job);
+}
+int zkmi_msm_wait(zkmi_msm_job* job, uint64_t* out_affine) { return msm_wait(job, out_affine); }
 int zkmi_msm_set_window(zkmi_ctx* ctx, int c) {
   if (c != 0 && (c < 4 || c > 17)) {
     set_error("window %d outside [4, 17]", c);

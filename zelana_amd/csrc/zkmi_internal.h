@@ -53,6 +53,7 @@ struct zkmi_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   zk::Workspace ws;
+  std::vector<std::pair<void*, size_t>> pinned_free;  // pool of pinned host buffers
   zk::KernelTimer timer;
   int msm_window = 0;  // 0 = auto
   int num_cus = 256;
@@ -79,12 +80,25 @@ struct ScopedKernelTimer {
   ~ScopedKernelTimer() { timer_end(ctx, name, ev); }
 };
 
+// pinned host staging buffers (pooled per context)
+int ctx_pinned_get(zkmi_ctx* ctx, size_t bytes, void** out);
+void ctx_pinned_put(zkmi_ctx* ctx, void* p);
+
 // MSM entry (msm.hip): device scalars, result canonical affine
 int msm_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                uint64_t* out_affine);
+int msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+               zkmi_msm_job** job);
+int msm_wait(zkmi_msm_job* job, uint64_t* out_affine);
+void msm_job_free(zkmi_msm_job* job);
 int bases_upload(zkmi_ctx* ctx, int g2, const uint64_t* host_affine, size_t n, zkmi_bases** out);
 // convert canonical affine already in device memory (n points) into a bases set
 int bases_from_device_canon(zkmi_ctx* ctx, int g2, const uint32_t* d_canon, size_t n, zkmi_bases** out);
+
+// synthetic inputs generated in HBM (bench) and canonical export (checks)
+int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t n, zkmi_bases** out);
+int bases_export(const zkmi_bases* b, uint64_t* host_out);
+int scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_out);
 
 // NTT entry (ntt.hip): in-place on device, natural order
 int ntt_device(zkmi_ctx* ctx, uint32_t* d_data, uint32_t log_n, int inverse, int coset);

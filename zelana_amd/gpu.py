@@ -46,13 +46,24 @@ class DeviceBuffer:
 
 
 class Bases:
-    def __init__(self, ctx: "Context", points: np.ndarray, g2: bool):
+    def __init__(self, ctx: "Context", points, g2: bool, *, generate_seed=None, n=None):
+        if generate_seed is not None:
+            self.ctx, self.g2, self.n = ctx, g2, n
+            self.h = vp()
+            f = lib().zkmi_bases_generate_g2 if g2 else lib().zkmi_bases_generate_g1
+            check(f(ctx.h, generate_seed, n, ctypes.byref(self.h)), "zkmi_bases_generate")
+            return
         pts = np.ascontiguousarray(points, dtype=np.uint64)
         assert pts.ndim == 2 and pts.shape[1] == (16 if g2 else 8)
         self.ctx, self.g2, self.n = ctx, g2, pts.shape[0]
         self.h = vp()
         f = lib().zkmi_bases_create_g2 if g2 else lib().zkmi_bases_create_g1
         check(f(ctx.h, _p64(pts), self.n, ctypes.byref(self.h)), "zkmi_bases_create")
+
+    def export(self):
+        out = np.zeros((self.n, 16 if self.g2 else 8), np.uint64)
+        check(lib().zkmi_bases_export(self.h, _p64(out)), "zkmi_bases_export")
+        return out
 
     def __del__(self):
         try:
@@ -104,6 +115,14 @@ class Context:
     def bases_g2(self, points):
         return Bases(self, points, True)
 
+    def bases_generate(self, seed: int, n: int, g2: bool = False):
+        return Bases(self, None, g2, generate_seed=seed, n=n)
+
+    def scalars_generate(self, seed: int, n: int) -> DeviceBuffer:
+        buf = DeviceBuffer(self, max(1, n) * 32)
+        check(lib().zkmi_scalars_generate(self.h, seed, n, buf.ptr), "zkmi_scalars_generate")
+        return buf
+
     def msm(self, bases: Bases, scalars, offset: int = 0):
         out = np.zeros(16 if bases.g2 else 8, np.uint64)
         if isinstance(scalars, DeviceBuffer):
@@ -114,6 +133,18 @@ class Context:
             sc = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
             f = lib().zkmi_msm_g2 if bases.g2 else lib().zkmi_msm_g1
             check(f(self.h, bases.h, offset, _p64(sc), sc.shape[0], _p64(out)), "zkmi_msm")
+        return out
+
+    def msm_submit(self, bases: Bases, dscalars: DeviceBuffer, n: int, offset: int = 0):
+        """Queue an MSM; returns a job handle for msm_wait (host epilogue)."""
+        job = vp()
+        check(lib().zkmi_msm_submit(self.h, bases.h, offset, dscalars.ptr, n, ctypes.byref(job)), "zkmi_msm_submit")
+        return (job, bases.g2)
+
+    def msm_wait(self, job):
+        h, g2 = job
+        out = np.zeros(16 if g2 else 8, np.uint64)
+        check(lib().zkmi_msm_wait(h, _p64(out)), "zkmi_msm_wait")
         return out
 
     def msm_device_n(self, bases: Bases, dscalars: DeviceBuffer, n: int, offset: int = 0):
