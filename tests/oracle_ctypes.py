@@ -52,7 +52,7 @@ def lib():
         L.oracle_pk_free.argtypes = [vp]
         L.oracle_pk_sizes.argtypes = [vp, u64p]
         L.oracle_pk_serialize.restype = ctypes.c_size_t
-        L.oracle_pk_serialize.argtypes = [vp, ctypes.c_int, u8p, ctypes.c_size_t]
+        L.oracle_pk_serialize.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
         L.oracle_vk_serialize.restype = ctypes.c_size_t
         L.oracle_vk_serialize.argtypes = [vp, ctypes.c_int, u8p, ctypes.c_size_t]
         L.oracle_groth16_prove.argtypes = [vp, vp, u64p, vp, u64p, ctypes.c_int, u64p, u64p, u64p, u64p]

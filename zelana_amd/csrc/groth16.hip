@@ -1,0 +1,744 @@
+// groth16.hip — Groth16 proving over BN254 on gfx950.  Replaces, behind the C
+// ABI, what Zelana's Groth16Prover delegates to arkworks 0.5.0:
+//   * ProvingKey::deserialize_compressed (core/src/sequencer/settlement/
+//     prover.rs:263-267): point decompression + on-curve / subgroup validation
+//     run as GPU kernels, queries stay resident in HBM (zkmi_pk_load);
+//   * LibsnarkReduction::witness_map_from_matrices: sparse
+//     mat-vec + 7 radix-2 transforms + pointwise QAP step, chained DIF/DIT so no
+//     bit-reversal pass is ever needed (h comes out bit-reversed and h_query is
+//     stored bit-reversed at load time);
+//   * create_proof_with_assignment (§8a a4): 4 G1 + 1 G2 MSMs submitted back to
+//     back (host epilogue of one overlaps the next's kernels), then the
+//     O(1) assembly A = alpha + sum z a + r delta, B = beta + sum z b + s delta,
+//     C = s A + r B1 - r s delta + sum_aux z l + sum h h_query on the host.
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "dev_io.h"
+#include "ec.h"
+#include "zkmi_internal.h"
+
+struct zkmi_pk {
+  zkmi_ctx* ctx;
+  uint64_t n = 0, num_instance = 0, num_witness = 0;
+  uint32_t log_n = 0;
+  uint64_t alpha_g1[8], beta_g1[8], delta_g1[8];
+  uint64_t beta_g2[16], gamma_g2[16], delta_g2[16];
+  std::vector<uint64_t> gamma_abc;  // num_instance x 8
+  uint64_t a0[8], b1_0[8], b2_0[16];
+  zkmi_bases *a_query = nullptr, *b_g1_query = nullptr, *b_g2_query = nullptr, *h_query_rev = nullptr,
+             *l_query = nullptr;
+  std::vector<uint8_t> vk_compressed;
+};
+
+namespace zk {
+
+int ntt_raw(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit);
+int ntt_bitrev(zkmi_ctx* ctx, uint32_t* d, uint32_t logn);
+
+// ------------------------------------------------------------ decoding
+__constant__ uint32_t FQ_MOD32[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                                     0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+__constant__ uint32_t G2B32_C0[8] = {0x24a138e5u, 0x3267e6dcu, 0x59dbefa3u, 0xb5b4c5e5u,
+                                     0x1be06ac3u, 0x81be1899u, 0xceb8aaaeu, 0x2b149d40u};
+__constant__ uint32_t G2B32_C1[8] = {0x85c315d2u, 0xe4a2bd06u, 0xe52d1852u, 0xa74fa084u,
+                                     0xeed8fdf4u, 0xcd2cafadu, 0x3af0fed4u, 0x009713b0u};
+
+__device__ __forceinline__ bool lt_q_words(const uint32_t* w) {
+  for (int i = 7; i >= 0; i--) {
+    if (w[i] != FQ_MOD32[i]) return w[i] < FQ_MOD32[i];
+  }
+  return false;
+}
+// compare two fully reduced values limb-wise: -1, 0, 1
+__device__ __forceinline__ int fe_cmp(const Fe& a, const Fe& b) {
+  for (int i = NL - 1; i >= 0; i--) {
+    if (a.v[i] != b.v[i]) return a.v[i] > b.v[i] ? 1 : -1;
+  }
+  return 0;
+}
+__device__ Fe fq_pow64(const Fe& a, const uint64_t e[4]) { return pow<FqP>(a, e); }
+__device__ Fe2 f2_pow(const Fe2& a, const uint64_t e[4]) {
+  Fe2 r = f2_one();
+  for (int i = 255; i >= 0; i--) {
+    r = f2_sqr(r);
+    if ((e[i >> 6] >> (i & 63)) & 1) r = f2_mul(r, a);
+  }
+  return r;
+}
+__device__ bool f2_eq(const Fe2& a, const Fe2& b) { return eq<FqP>(a.c0, b.c0) && eq<FqP>(a.c1, b.c1); }
+// canonical (reduced, non-Montgomery) value of a Montgomery element
+__device__ Fe canon_q(const Fe& a) { return from_mont<FqP>(a); }
+
+// sqrt in Fq2 for q = 3 mod 4 (Adj & Rodriguez-Henriquez, Alg. 9); which root
+// is returned does not matter (the caller picks y or -y by the flag)
+__device__ bool f2_sqrt(const Fe2& a, Fe2& out) {
+  const uint64_t e34[4] = {0x4f082305b61f3f51ull, 0x65e05aa45a1c72a3ull, 0x6e14116da0605617ull,
+                           0x0c19139cb84c680aull};  // (q-3)/4
+  const uint64_t e12[4] = {0x9e10460b6c3e7ea3ull, 0xcbc0b548b438e546ull, 0xdc2822db40c0ac2eull,
+                           0x183227397098d014ull};  // (q-1)/2
+  Fe2 a1 = f2_pow(a, e34);
+  Fe2 alpha = f2_mul(a1, f2_mul(a1, a));
+  Fe2 conj = {alpha.c0, neg<FqP>(alpha.c1)};
+  Fe2 a0 = f2_mul(conj, alpha);
+  Fe2 m1 = {neg<FqP>(one<FqP>()), fe_zero()};
+  if (f2_eq(a0, m1)) return false;
+  Fe2 x0 = f2_mul(a1, a);
+  if (f2_eq(alpha, m1)) {
+    out = {neg<FqP>(x0.c1), x0.c0};
+  } else {
+    Fe2 b = {add<FqP>(alpha.c0, one<FqP>()), alpha.c1};
+    out = f2_mul(f2_pow(b, e12), x0);
+  }
+  return f2_eq(f2_sqr(out), a);
+}
+
+// raw arkworks encodings (SWFlags in the top two bits of the last byte) ->
+// canonical affine words; bad |= 1 on any invalid point
+__global__ void __launch_bounds__(256) k_decode_g1(const uint32_t* __restrict__ raw, size_t n, int compressed,
+                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ bad) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int words = compressed ? 8 : 16;
+  uint32_t w[16];
+  for (int k = 0; k < words; k++) w[k] = raw[i * words + k];
+  uint32_t flags = w[words - 1] >> 30;
+  w[words - 1] &= 0x3FFFFFFFu;
+  uint32_t* o = out + i * 16;
+  if (flags & 1) {  // PointAtInfinity (bit 6 of the last byte)
+    for (int k = 0; k < 16; k++) o[k] = 0;
+    return;
+  }
+  if (!lt_q_words(w) || (!compressed && !lt_q_words(w + 8))) {
+    atomicOr(bad, 1u);
+    return;
+  }
+  Fe x = to_mont<FqP>(unpack(w));
+  Fe rhs = add<FqP>(mul<FqP>(sqr<FqP>(x), x), to_mont<FqP>(Fe{{3, 0, 0, 0, 0, 0, 0, 0, 0}}));
+  Fe yc;
+  if (compressed) {
+    const uint64_t e14[4] = {0x4f082305b61f3f52ull, 0x65e05aa45a1c72a3ull, 0x6e14116da0605617ull,
+                             0x0c19139cb84c680aull};  // (q+1)/4
+    Fe y = fq_pow64(rhs, e14);
+    if (!eq<FqP>(sqr<FqP>(y), rhs)) {
+      atomicOr(bad, 1u);
+      return;
+    }
+    Fe c = canon_q(y), nc = canon_q(neg<FqP>(y));
+    bool larger_is_c = fe_cmp(c, nc) > 0;
+    bool want_larger = (flags >> 1) & 1;  // YIsNegative <=> y > -y
+    yc = (larger_is_c == want_larger) ? c : nc;
+  } else {
+    Fe y = to_mont<FqP>(unpack(w + 8));
+    if (!eq<FqP>(sqr<FqP>(y), rhs)) {
+      atomicOr(bad, 1u);
+      return;
+    }
+    yc = canon_q(y);
+  }
+  st_fe(o, canon_q(x));
+  st_fe(o + 8, yc);
+}
+
+__constant__ uint64_t FR_MOD64_G[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
+                                       0x30644e72e131a029ull};
+
+__global__ void __launch_bounds__(256) k_decode_g2(const uint32_t* __restrict__ raw, size_t n, int compressed,
+                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ bad) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int words = compressed ? 16 : 32;
+  uint32_t w[32];
+  for (int k = 0; k < words; k++) w[k] = raw[i * words + k];
+  uint32_t flags = w[words - 1] >> 30;
+  w[words - 1] &= 0x3FFFFFFFu;
+  uint32_t* o = out + i * 32;
+  if (flags & 1) {
+    for (int k = 0; k < 32; k++) o[k] = 0;
+    return;
+  }
+  for (int c = 0; c < words / 8; c++) {
+    if (!lt_q_words(w + 8 * c)) {
+      atomicOr(bad, 1u);
+      return;
+    }
+  }
+  Fe2 x = {to_mont<FqP>(unpack(w)), to_mont<FqP>(unpack(w + 8))};
+  Fe2 b = {to_mont<FqP>(ldc_fe(G2B32_C0)), to_mont<FqP>(ldc_fe(G2B32_C1))};
+  Fe2 rhs = f2_add(f2_mul(f2_sqr(x), x), b);
+  Fe2 y;
+  if (compressed) {
+    if (!f2_sqrt(rhs, y)) {
+      atomicOr(bad, 1u);
+      return;
+    }
+    Fe2 ny = f2_neg(y);
+    Fe yc0 = canon_q(y.c0), yc1 = canon_q(y.c1), nc0 = canon_q(ny.c0), nc1 = canon_q(ny.c1);
+    int cmp = fe_cmp(yc1, nc1);
+    if (cmp == 0) cmp = fe_cmp(yc0, nc0);  // arkworks Fq2 order: c1 first
+    bool larger_is_y = cmp > 0;
+    bool want_larger = (flags >> 1) & 1;
+    if (larger_is_y != want_larger) y = ny;
+  } else {
+    y = {to_mont<FqP>(unpack(w + 16)), to_mont<FqP>(unpack(w + 24))};
+    if (!f2_eq(f2_sqr(y), rhs)) {
+      atomicOr(bad, 1u);
+      return;
+    }
+  }
+  // prime-order subgroup check: [r] P == O
+  Aff<Fq2Ops> P = {x, y};
+  Xyzz<Fq2Ops> acc = xyzz_inf<Fq2Ops>();
+  for (int bit = 253; bit >= 0; bit--) {
+    acc = xyzz_dbl(acc);
+    if ((FR_MOD64_G[bit >> 6] >> (bit & 63)) & 1) acc = xyzz_madd(acc, P);
+  }
+  if (!xyzz_is_inf(acc)) {
+    atomicOr(bad, 2u);
+    return;
+  }
+  st_fe(o, canon_q(x.c0));
+  st_fe(o + 8, canon_q(x.c1));
+  st_fe(o + 16, canon_q(y.c0));
+  st_fe(o + 24, canon_q(y.c1));
+}
+
+// out[p] = in[rev(p)]  (G1 canonical affine, 16 words), p < cnt
+__global__ void __launch_bounds__(256) k_permute_rev(const uint32_t* __restrict__ in, uint32_t logn, size_t cnt,
+                                                     uint32_t* __restrict__ out) {
+  size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (p >= cnt) return;
+  size_t src = logn ? (__brev((uint32_t)p) >> (32 - logn)) : 0;
+  for (int k = 0; k < 16; k++) out[p * 16 + k] = in[src * 16 + k];
+}
+
+// ------------------------------------------------------------ witness map
+// z (canonical) -> Montgomery copy for the mat-vec
+__global__ void __launch_bounds__(256) k_to_mont_fr(const uint32_t* __restrict__ z, size_t n, uint32_t* __restrict__ zm) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  st_fe(zm + i * 8, to_mont<FrP>(ld_fe(z + i * 8)));
+}
+// rows i < m: out[i] = sum_k val_k * z[col_k]  (val canonical, z Montgomery ->
+// canonical product); rows m <= i < m + l of A copy z (inputs appended to A
+// only); the rest of the domain is zero.  (evaluate_constraint, §8a a5)
+__global__ void __launch_bounds__(256) k_matvec(const uint64_t* __restrict__ rowptr, const uint64_t* __restrict__ col,
+                                                const uint32_t* __restrict__ val, const uint32_t* __restrict__ zm,
+                                                const uint32_t* __restrict__ zc, size_t m, size_t l, size_t n,
+                                                int is_a, uint32_t* __restrict__ out) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fe acc = fe_zero();
+  if (i < m) {
+    for (uint64_t k = rowptr[i]; k < rowptr[i + 1]; k++) {
+      Fe t = mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8));
+      acc = add<FrP>(acc, t);
+    }
+  } else if (is_a && i < m + l) {
+    acc = ld_fe(zc + (i - m) * 8);
+  }
+  st_fe(out + i * 8, acc);
+}
+// powers table: tab[x] = c * base^(x * step) for x < cnt (Montgomery), runs of 64
+__global__ void __launch_bounds__(256) k_pow_table(uint32_t* __restrict__ tab, uint32_t cnt, const uint32_t* base_c,
+                                                   uint64_t step, const uint32_t* mult_m) {
+  uint32_t run = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t x0 = run * 64;
+  if (x0 >= cnt) return;
+  Fe b = to_mont<FrP>(ld_fe(base_c));
+  Fe bs = one<FrP>();
+  {
+    Fe bb = b;
+    uint64_t e = step;
+    while (e) {
+      if (e & 1) bs = mul<FrP>(bs, bb);
+      bb = sqr<FrP>(bb);
+      e >>= 1;
+    }
+  }
+  Fe cur = one<FrP>();
+  {
+    Fe bb = bs;
+    uint64_t e = x0;
+    while (e) {
+      if (e & 1) cur = mul<FrP>(cur, bb);
+      bb = sqr<FrP>(bb);
+      e >>= 1;
+    }
+  }
+  if (mult_m) cur = mul<FrP>(cur, ld_fe(mult_m));
+  for (uint32_t k = 0; k < 64 && x0 + k < cnt; k++) {
+    st_fe(tab + (size_t)(x0 + k) * 8, reduce<FrP>(cur));
+    cur = mul<FrP>(cur, bs);
+  }
+}
+// data[p] *= lo[e & (2^kb - 1)] * hi[e >> kb] with e = rev(p)  (coset powers in
+// bit-reversed layout; hi carries the constant factor)
+__global__ void __launch_bounds__(256) k_scale_rev(uint32_t* __restrict__ data, uint32_t logn,
+                                                   const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi,
+                                                   uint32_t kb, int final_reduce) {
+  size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (p >= (1ull << logn)) return;
+  uint32_t e = logn ? (__brev((uint32_t)p) >> (32 - logn)) : 0;
+  Fe v = mul<FrP>(ld_fe(data + p * 8), ld_fe(lo + (size_t)(e & ((1u << kb) - 1)) * 8));
+  v = mul<FrP>(v, ld_fe(hi + (size_t)(e >> kb) * 8));
+  st_fe(data + p * 8, final_reduce ? reduce<FrP>(v) : v);
+}
+// a = (a * b - c) * vinv  (natural order, coset evaluations).  a, b, c are in
+// value form (the data never enter Montgomery form), so the Montgomery product
+// a*b*R^-1 is brought back with one multiplication by R^2.
+__global__ void __launch_bounds__(256) k_qap_combine(uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                                     const uint32_t* __restrict__ c, size_t n,
+                                                     const uint32_t* __restrict__ vinv_m) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fe ab = mul<FrP>(mul<FrP>(ld_fe(a + i * 8), ld_fe(b + i * 8)), fe_const<FrP>(FrP::R2));
+  Fe t = sub<FrP>(ab, ld_fe(c + i * 8));
+  st_fe(a + i * 8, mul<FrP>(t, ld_fe(vinv_m)));
+}
+// scalar constants for a domain: [n^-1 (canon), (g^n - 1)^-1 (Montgomery)]
+__global__ void k_domain_consts(uint32_t logn, uint32_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const uint64_t rm2[4] = {0x43e1f593efffffffull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
+                           0x30644e72e131a029ull};  // r - 2
+  Fe two = to_mont<FrP>(Fe{{2, 0, 0, 0, 0, 0, 0, 0, 0}});
+  Fe nn = one<FrP>();
+  for (uint32_t k = 0; k < logn; k++) nn = mul<FrP>(nn, two);
+  Fe ninv = pow<FrP>(nn, rm2);
+  st_fe(out, from_mont<FrP>(ninv));
+  Fe g = to_mont<FrP>(Fe{{5, 0, 0, 0, 0, 0, 0, 0, 0}});
+  Fe gn = g;
+  for (uint32_t k = 0; k < logn; k++) gn = sqr<FrP>(gn);
+  Fe v = sub<FrP>(gn, one<FrP>());
+  st_fe(out + 8, pow<FrP>(v, rm2));
+}
+
+static const uint32_t G5[8] = {5, 0, 0, 0, 0, 0, 0, 0};
+static const uint32_t GINV5[8] = {0xc6666667u, 0xe7f3fbd4u, 0xca4a2d06u, 0xa9ae5ce9u,
+                                  0x33cd568bu, 0x49b9b57cu, 0x5a13d9aau, 0x135b5294u};
+constexpr uint32_t COSET_KB = 14;
+
+// per-log_n constants and coset power tables, cached in the context
+struct DomainCache {
+  uint32_t* consts;  // [n^-1 canon | vinv mont]
+  uint32_t *lo_g, *hi_g, *lo_gi, *hi_gi;
+};
+static int domain_cache(zkmi_ctx* ctx, uint32_t logn, DomainCache* dc) {
+  char nm[64];
+  snprintf(nm, sizeof(nm), "g16_consts_%u", logn);
+  bool fresh = ctx->ws.bufs.find(nm) == ctx->ws.bufs.end();
+  ZK_TRY(ctx->ws.get(nm, 64, (void**)&dc->consts));
+  uint32_t nhi = std::max<uint32_t>(1, (uint32_t)(((1ull << logn) + (1u << COSET_KB) - 1) >> COSET_KB));
+  uint32_t nlo = 1u << COSET_KB;
+  const char* names[4] = {"lo_g", "hi_g", "lo_gi", "hi_gi"};
+  uint32_t** ptrs[4] = {&dc->lo_g, &dc->hi_g, &dc->lo_gi, &dc->hi_gi};
+  for (int t = 0; t < 4; t++) {
+    char tn[64];
+    snprintf(tn, sizeof(tn), "g16_%s_%u", names[t], logn);
+    ZK_TRY(ctx->ws.get(tn, (size_t)((t & 1) ? nhi : nlo) * 32, (void**)ptrs[t]));
+  }
+  if (fresh) {
+    hipStream_t st = ctx->stream;
+    k_domain_consts<<<1, 64, 0, st>>>(logn, dc->consts);
+    uint32_t *cg, *cgi;
+    ZK_TRY(ctx->ws.get("g16_gconst", 64, (void**)&cg));
+    cgi = cg + 8;
+    ZK_HIP(hipMemcpyAsync(cg, G5, 32, hipMemcpyHostToDevice, st));
+    ZK_HIP(hipMemcpyAsync(cgi, GINV5, 32, hipMemcpyHostToDevice, st));
+    // n^-1 as a Montgomery multiplier for the hi tables: convert via a tiny
+    // table build with step 0 (tab[x] = n^-1 * base^0) is avoided: fold it in
+    // through mult_m = Montgomery(n^-1) computed by k_to_mont_fr.
+    uint32_t* ninv_m;
+    ZK_TRY(ctx->ws.get("g16_ninv_m", 32, (void**)&ninv_m));
+    k_to_mont_fr<<<1, 64, 0, st>>>(dc->consts, 1, ninv_m);
+    unsigned glo = (nlo / 64 + 255) / 256, ghi = ((nhi + 63) / 64 + 255) / 256;
+    k_pow_table<<<glo, 256, 0, st>>>(dc->lo_g, nlo, cg, 1, nullptr);
+    k_pow_table<<<ghi, 256, 0, st>>>(dc->hi_g, nhi, cg, 1ull << COSET_KB, ninv_m);
+    k_pow_table<<<glo, 256, 0, st>>>(dc->lo_gi, nlo, cgi, 1, nullptr);
+    k_pow_table<<<ghi, 256, 0, st>>>(dc->hi_gi, nhi, cgi, 1ull << COSET_KB, ninv_m);
+    ZK_HIP(hipGetLastError());
+    ZK_HIP(hipStreamSynchronize(st));
+  }
+  return 0;
+}
+
+struct DevR1CS {
+  uint64_t *rp[3], *col[3];
+  uint32_t* val[3];
+};
+static int upload_r1cs(zkmi_ctx* ctx, const zkmi_r1cs* cs, DevR1CS* d) {
+  const uint64_t* rps[3] = {cs->a_rowptr, cs->b_rowptr, cs->c_rowptr};
+  const uint64_t* cols[3] = {cs->a_col, cs->b_col, cs->c_col};
+  const uint64_t* vals[3] = {cs->a_val, cs->b_val, cs->c_val};
+  const char* nm[3] = {"a", "b", "c"};
+  size_t m = cs->num_constraints, nv = cs->num_instance + cs->num_witness;
+  for (int t = 0; t < 3; t++) {
+    if (!rps[t] || (m && (!cols[t] || !vals[t]))) {
+      set_error("r1cs: matrix %s missing", nm[t]);
+      return ZKMI_EINVAL;
+    }
+    uint64_t nnz = rps[t][m];
+    for (size_t i = 0; i < m; i++) {
+      if (rps[t][i] > rps[t][i + 1]) {
+        set_error("r1cs: matrix %s rowptr not monotone at %zu", nm[t], i);
+        return ZKMI_EINVAL;
+      }
+    }
+    for (uint64_t k = 0; k < nnz; k++) {
+      if (cols[t][k] >= nv) {
+        set_error("r1cs: matrix %s column %llu >= num_variables %zu", nm[t], (unsigned long long)cols[t][k], nv);
+        return ZKMI_EINVAL;
+      }
+    }
+    char b1[32], b2[32], b3[32];
+    snprintf(b1, 32, "r1cs_rp_%s", nm[t]);
+    snprintf(b2, 32, "r1cs_col_%s", nm[t]);
+    snprintf(b3, 32, "r1cs_val_%s", nm[t]);
+    ZK_TRY(ctx->ws.get(b1, (m + 1) * 8, (void**)&d->rp[t]));
+    ZK_TRY(ctx->ws.get(b2, std::max<uint64_t>(1, nnz) * 8, (void**)&d->col[t]));
+    ZK_TRY(ctx->ws.get(b3, std::max<uint64_t>(1, nnz) * 32, (void**)&d->val[t]));
+    ZK_HIP(hipMemcpyAsync(d->rp[t], rps[t], (m + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (nnz) {
+      ZK_HIP(hipMemcpyAsync(d->col[t], cols[t], nnz * 8, hipMemcpyHostToDevice, ctx->stream));
+      ZK_HIP(hipMemcpyAsync(d->val[t], vals[t], nnz * 32, hipMemcpyHostToDevice, ctx->stream));
+    }
+  }
+  return 0;
+}
+
+static uint32_t domain_log(size_t need) {
+  uint32_t k = 0;
+  while (((size_t)1 << k) < need) k++;
+  return k;
+}
+
+// h (bit-reversed layout, canonical, n elements) into d_h from device z
+static int witness_map_dev(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint32_t* d_z, uint32_t logn, uint32_t* d_h) {
+  hipStream_t st = ctx->stream;
+  size_t m = cs->num_constraints, l = cs->num_instance, nv = l + cs->num_witness;
+  size_t n = (size_t)1 << logn;
+  DevR1CS dr;
+  ZK_TRY(upload_r1cs(ctx, cs, &dr));
+  DomainCache dc;
+  ZK_TRY(domain_cache(ctx, logn, &dc));
+  uint32_t *zm, *b, *c;
+  ZK_TRY(ctx->ws.get("wm_zm", nv * 32, (void**)&zm));
+  ZK_TRY(ctx->ws.get("wm_b", n * 32, (void**)&b));
+  ZK_TRY(ctx->ws.get("wm_c", n * 32, (void**)&c));
+  uint32_t* a = d_h;
+  unsigned gn = (unsigned)((n + 255) / 256);
+  {
+    ScopedKernelTimer tm(ctx, "g16_matvec");
+    k_to_mont_fr<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(d_z, nv, zm);
+    k_matvec<<<gn, 256, 0, st>>>(dr.rp[0], dr.col[0], dr.val[0], zm, d_z, m, l, n, 1, a);
+    k_matvec<<<gn, 256, 0, st>>>(dr.rp[1], dr.col[1], dr.val[1], zm, d_z, m, l, n, 0, b);
+    k_matvec<<<gn, 256, 0, st>>>(dr.rp[2], dr.col[2], dr.val[2], zm, d_z, m, l, n, 0, c);
+    ZK_HIP(hipGetLastError());
+  }
+  // evaluations -> coefficients (DIF, bit-reversed) -> * n^-1 g^i -> coset
+  // evaluations (DIT, natural)
+  uint32_t* vecs[3] = {a, b, c};
+  for (int t = 0; t < 3; t++) {
+    ZK_TRY(ntt_raw(ctx, vecs[t], logn, 1, false));
+    {
+      ScopedKernelTimer tm(ctx, "g16_scale");
+      k_scale_rev<<<gn, 256, 0, st>>>(vecs[t], logn, dc.lo_g, dc.hi_g, COSET_KB, 0);
+    }
+    ZK_TRY(ntt_raw(ctx, vecs[t], logn, 0, true));
+  }
+  {
+    ScopedKernelTimer tm(ctx, "g16_qap");
+    k_qap_combine<<<gn, 256, 0, st>>>(a, b, c, n, dc.consts + 8);
+  }
+  // coset evaluations -> coefficients: DIF inverse, * n^-1 g^-i, reduce
+  ZK_TRY(ntt_raw(ctx, a, logn, 1, false));
+  {
+    ScopedKernelTimer tm(ctx, "g16_scale");
+    k_scale_rev<<<gn, 256, 0, st>>>(a, logn, dc.lo_gi, dc.hi_gi, COSET_KB, 1);
+  }
+  ZK_HIP(hipGetLastError());
+  return 0;
+}
+
+static int check_cs(const zkmi_r1cs* cs) {
+  if (!cs || cs->num_instance < 1) {
+    set_error("r1cs: need at least the One variable (num_instance >= 1)");
+    return ZKMI_EINVAL;
+  }
+  return 0;
+}
+
+int witness_map_host(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t* z, uint64_t* h_out) {
+  ZK_TRY(check_cs(cs));
+  size_t nv = cs->num_instance + cs->num_witness;
+  uint32_t logn = domain_log(cs->num_constraints + cs->num_instance);
+  if (logn > 28) {
+    set_error("witness map: domain 2^%u exceeds Fr two-adicity", logn);
+    return ZKMI_EINVAL;
+  }
+  size_t n = (size_t)1 << logn;
+  uint32_t *dz, *dh;
+  ZK_TRY(ctx->ws.get("g16_z", nv * 32, (void**)&dz));
+  ZK_TRY(ctx->ws.get("g16_h", n * 32, (void**)&dh));
+  ZK_HIP(hipMemcpyAsync(dz, z, nv * 32, hipMemcpyHostToDevice, ctx->stream));
+  ZK_TRY(witness_map_dev(ctx, cs, dz, logn, dh));
+  ZK_TRY(ntt_bitrev(ctx, dh, logn));  // natural order for the caller
+  ZK_HIP(hipMemcpyAsync(h_out, dh, n * 32, hipMemcpyDeviceToHost, ctx->stream));
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  return timer_flush(ctx);
+}
+
+// ------------------------------------------------------------ pk load
+struct Rd {
+  const uint8_t* p;
+  size_t len, off = 0;
+  bool ok = true;
+  const uint8_t* take(size_t k) {
+    if (!ok || off + k > len) {
+      ok = false;
+      return nullptr;
+    }
+    const uint8_t* r = p + off;
+    off += k;
+    return r;
+  }
+  uint64_t u64() {
+    const uint8_t* b = take(8);
+    if (!b) return 0;
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v |= (uint64_t)b[i] << (8 * i);
+    return v;
+  }
+};
+
+// decode `cnt` raw points (contiguous bytes) on the GPU -> canonical affine in d_out
+static int decode_points(zkmi_ctx* ctx, int g2, const uint8_t* raw, size_t cnt, int compressed, uint32_t* d_out) {
+  if (!cnt) return 0;
+  size_t psz = (g2 ? 64 : 32) * (compressed ? 1 : 2);
+  uint32_t *d_raw, *d_bad;
+  ZK_TRY(ctx->ws.get("pk_raw", cnt * psz, (void**)&d_raw));
+  ZK_TRY(ctx->ws.get("pk_bad", 4, (void**)&d_bad));
+  ZK_HIP(hipMemsetAsync(d_bad, 0, 4, ctx->stream));
+  ZK_HIP(hipMemcpyAsync(d_raw, raw, cnt * psz, hipMemcpyHostToDevice, ctx->stream));
+  unsigned grid = (unsigned)((cnt + 255) / 256);
+  {
+    ScopedKernelTimer tm(ctx, g2 ? "pk_decode_g2" : "pk_decode_g1");
+    if (g2) k_decode_g2<<<grid, 256, 0, ctx->stream>>>(d_raw, cnt, compressed, d_out, d_bad);
+    else k_decode_g1<<<grid, 256, 0, ctx->stream>>>(d_raw, cnt, compressed, d_out, d_bad);
+    ZK_HIP(hipGetLastError());
+  }
+  uint32_t bad = 0;
+  ZK_HIP(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, ctx->stream));
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  if (bad) {
+    set_error("pk: invalid %s point encoding (%s)", g2 ? "G2" : "G1",
+              (bad & 2) ? "not in the prime-order subgroup" : "not on curve / non-canonical");
+    return ZKMI_EPOINT;
+  }
+  return 0;
+}
+static int decode_to_host(zkmi_ctx* ctx, int g2, const uint8_t* raw, size_t cnt, int compressed, uint64_t* host) {
+  if (!cnt) return 0;
+  uint32_t* d;
+  ZK_TRY(ctx->ws.get("pk_small", cnt * (g2 ? 128 : 64), (void**)&d));
+  ZK_TRY(decode_points(ctx, g2, raw, cnt, compressed, d));
+  ZK_HIP(hipMemcpy(host, d, cnt * (g2 ? 128 : 64), hipMemcpyDeviceToHost));
+  return 0;
+}
+static int decode_to_bases(zkmi_ctx* ctx, int g2, const uint8_t* raw, size_t cnt, int compressed, zkmi_bases** out,
+                           uint32_t permute_logn = 0, size_t keep = (size_t)-1) {
+  uint32_t* d;
+  size_t pw = g2 ? 32 : 16;
+  ZK_TRY(ctx->ws.get("pk_canon", std::max<size_t>(1, cnt) * pw * 4, (void**)&d));
+  ZK_TRY(decode_points(ctx, g2, raw, cnt, compressed, d));
+  if (permute_logn) {
+    uint32_t* d2;
+    ZK_TRY(ctx->ws.get("pk_perm", std::max<size_t>(1, keep) * pw * 4, (void**)&d2));
+    // positions p < keep take h_query[rev(p)] (rev(p) < cnt for p < keep)
+    k_permute_rev<<<(unsigned)((keep + 255) / 256), 256, 0, ctx->stream>>>(d, permute_logn, keep, d2);
+    ZK_HIP(hipGetLastError());
+    return bases_from_device_canon(ctx, g2, d2, keep, out);
+  }
+  return bases_from_device_canon(ctx, g2, d, cnt, out);
+}
+
+int pk_load(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, int compressed, zkmi_pk** out) {
+  *out = nullptr;
+  const size_t s1 = compressed ? 32 : 64, s2 = compressed ? 64 : 128;
+  Rd r{bytes, len};
+  const uint8_t* alpha = r.take(s1);
+  const uint8_t* g2s = r.take(3 * s2);  // beta, gamma, delta (G2)
+  uint64_t nabc = r.u64();
+  if (!r.ok || nabc == 0 || nabc > (1ull << 32)) {
+    set_error("pk: truncated verifying key");
+    return ZKMI_EINVAL;
+  }
+  const uint8_t* abc = r.take(nabc * s1);
+  size_t vk_end = r.off;
+  const uint8_t* bd1 = r.take(2 * s1);  // beta_g1, delta_g1
+  uint64_t na = r.u64();
+  const uint8_t* aq = r.ok ? r.take(na * s1) : nullptr;
+  uint64_t nb1 = r.u64();
+  const uint8_t* b1q = r.ok ? r.take(nb1 * s1) : nullptr;
+  uint64_t nb2 = r.u64();
+  const uint8_t* b2q = r.ok ? r.take(nb2 * s2) : nullptr;
+  uint64_t nh = r.u64();
+  const uint8_t* hq = r.ok ? r.take(nh * s1) : nullptr;
+  uint64_t nl = r.u64();
+  const uint8_t* lq = r.ok ? r.take(nl * s1) : nullptr;
+  if (!r.ok || r.off != len) {
+    set_error("pk: malformed ProvingKey encoding (parsed %zu of %zu bytes)", r.off, len);
+    return ZKMI_EINVAL;
+  }
+  uint64_t n = nh + 1;
+  if (na != nb1 || na != nb2 || na < nabc || nl != na - nabc || (n & (n - 1)) != 0) {
+    set_error("pk: inconsistent query lengths (a %llu b1 %llu b2 %llu h %llu l %llu ic %llu)",
+              (unsigned long long)na, (unsigned long long)nb1, (unsigned long long)nb2, (unsigned long long)nh,
+              (unsigned long long)nl, (unsigned long long)nabc);
+    return ZKMI_EINVAL;
+  }
+  zkmi_pk* pk = new zkmi_pk;
+  pk->ctx = ctx;
+  pk->n = n;
+  pk->log_n = domain_log(n);
+  pk->num_instance = nabc;
+  pk->num_witness = nl;
+  int rc = 0;
+  auto fail = [&](int code) {
+    zkmi_pk_destroy(pk);
+    return code;
+  };
+  uint64_t small1[3 * 8];
+  std::vector<uint8_t> s1buf(3 * s1);
+  memcpy(s1buf.data(), alpha, s1);
+  memcpy(s1buf.data() + s1, bd1, 2 * s1);
+  if ((rc = decode_to_host(ctx, 0, s1buf.data(), 3, compressed, small1))) return fail(rc);
+  memcpy(pk->alpha_g1, small1, 64);
+  memcpy(pk->beta_g1, small1 + 8, 64);
+  memcpy(pk->delta_g1, small1 + 16, 64);
+  uint64_t small2[3 * 16];
+  if ((rc = decode_to_host(ctx, 1, g2s, 3, compressed, small2))) return fail(rc);
+  memcpy(pk->beta_g2, small2, 128);
+  memcpy(pk->gamma_g2, small2 + 16, 128);
+  memcpy(pk->delta_g2, small2 + 32, 128);
+  pk->gamma_abc.resize(nabc * 8);
+  if ((rc = decode_to_host(ctx, 0, abc, nabc, compressed, pk->gamma_abc.data()))) return fail(rc);
+  if ((rc = decode_to_bases(ctx, 0, aq, na, compressed, &pk->a_query))) return fail(rc);
+  if ((rc = decode_to_bases(ctx, 0, b1q, nb1, compressed, &pk->b_g1_query))) return fail(rc);
+  if ((rc = decode_to_bases(ctx, 1, b2q, nb2, compressed, &pk->b_g2_query))) return fail(rc);
+  if ((rc = decode_to_bases(ctx, 0, hq, nh, compressed, &pk->h_query_rev, pk->log_n, nh))) return fail(rc);
+  if ((rc = decode_to_bases(ctx, 0, lq, nl, compressed, &pk->l_query))) return fail(rc);
+  // query[0] terms added outside the MSMs (calculate_coeff)
+  std::vector<uint64_t> tmp1(na * 8), tmp2(na * 16);
+  if ((rc = bases_export(pk->a_query, tmp1.data()))) return fail(rc);
+  memcpy(pk->a0, tmp1.data(), 64);
+  if ((rc = bases_export(pk->b_g1_query, tmp1.data()))) return fail(rc);
+  memcpy(pk->b1_0, tmp1.data(), 64);
+  if ((rc = bases_export(pk->b_g2_query, tmp2.data()))) return fail(rc);
+  memcpy(pk->b2_0, tmp2.data(), 128);
+  // compressed VK bytes (Groth16Prover::compute_vk_hash hashes these)
+  if (compressed) {
+    pk->vk_compressed.assign(bytes, bytes + vk_end);
+  } else {
+    std::vector<uint8_t> v(32 + 3 * 64 + 8 + nabc * 32);
+    g1_compress(pk->alpha_g1, v.data());
+    g2_compress(pk->beta_g2, v.data() + 32);
+    g2_compress(pk->gamma_g2, v.data() + 96);
+    g2_compress(pk->delta_g2, v.data() + 160);
+    for (int i = 0; i < 8; i++) v[224 + i] = (uint8_t)(nabc >> (8 * i));
+    for (uint64_t i = 0; i < nabc; i++) g1_compress(&pk->gamma_abc[i * 8], v.data() + 232 + i * 32);
+    pk->vk_compressed = v;
+  }
+  ZK_TRY(timer_flush(ctx));
+  *out = pk;
+  return 0;
+}
+
+// ------------------------------------------------------------ prove
+int groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const uint64_t* z, const uint64_t r[4],
+                  const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]) {
+  ZK_TRY(check_cs(cs));
+  size_t l = cs->num_instance, w = cs->num_witness, nv = l + w;
+  uint32_t logn = domain_log(cs->num_constraints + l);
+  if (l != pk->num_instance || w != pk->num_witness || ((size_t)1 << logn) != pk->n) {
+    set_error("prove: circuit shape (m %zu, l %zu, w %zu) does not match the proving key (n %llu, l %llu, w %llu)",
+              cs->num_constraints, l, w, (unsigned long long)pk->n, (unsigned long long)pk->num_instance,
+              (unsigned long long)pk->num_witness);
+    return ZKMI_EINVAL;
+  }
+  size_t n = pk->n;
+  uint32_t *dz, *dh;
+  ZK_TRY(ctx->ws.get("g16_z", nv * 32, (void**)&dz));
+  ZK_TRY(ctx->ws.get("g16_h", n * 32, (void**)&dh));
+  ZK_HIP(hipMemcpyAsync(dz, z, nv * 32, hipMemcpyHostToDevice, ctx->stream));
+  ZK_TRY(witness_map_dev(ctx, cs, dz, logn, dh));
+  // 5 MSMs back to back; each host epilogue overlaps the next one's kernels
+  zkmi_msm_job* jobs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint64_t h_acc[8], l_acc[8], a_acc[8], b1_acc[8], b2_acc[16];
+  int rc = 0;
+  rc = msm_submit(ctx, pk->h_query_rev, 0, dh, n - 1, &jobs[0]);
+  if (!rc) rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
+  if (!rc) rc = msm_wait(jobs[0], h_acc), jobs[0] = nullptr;
+  if (!rc) rc = msm_submit(ctx, pk->a_query, 1, dz + 8, nv - 1, &jobs[2]);
+  if (!rc) rc = msm_wait(jobs[1], l_acc), jobs[1] = nullptr;
+  if (!rc) rc = msm_submit(ctx, pk->b_g1_query, 1, dz + 8, nv - 1, &jobs[3]);
+  if (!rc) rc = msm_wait(jobs[2], a_acc), jobs[2] = nullptr;
+  if (!rc) rc = msm_submit(ctx, pk->b_g2_query, 1, dz + 8, nv - 1, &jobs[4]);
+  if (!rc) rc = msm_wait(jobs[3], b1_acc), jobs[3] = nullptr;
+  if (!rc) rc = msm_wait(jobs[4], b2_acc), jobs[4] = nullptr;
+  for (auto* j : jobs)
+    if (j) msm_job_free(j);
+  if (rc) return rc;
+  groth16_assemble(pk->alpha_g1, pk->beta_g1, pk->delta_g1, pk->beta_g2, pk->delta_g2, pk->a0, pk->b1_0, pk->b2_0,
+                   h_acc, l_acc, a_acc, b1_acc, b2_acc, r, s, a_out, b_out, c_out);
+  return 0;
+}
+
+}  // namespace zk
+
+using namespace zk;
+
+extern "C" {
+int zkmi_witness_map(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t* z, uint64_t* h_out) {
+  return witness_map_host(ctx, cs, z, h_out);
+}
+int zkmi_pk_load(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, int compressed, zkmi_pk** out) {
+  if (!ctx || !bytes || !out) {
+    set_error("zkmi_pk_load: null argument");
+    return ZKMI_EINVAL;
+  }
+  return pk_load(ctx, bytes, len, compressed, out);
+}
+void zkmi_pk_destroy(zkmi_pk* pk) {
+  if (!pk) return;
+  zkmi_bases_destroy(pk->a_query);
+  zkmi_bases_destroy(pk->b_g1_query);
+  zkmi_bases_destroy(pk->b_g2_query);
+  zkmi_bases_destroy(pk->h_query_rev);
+  zkmi_bases_destroy(pk->l_query);
+  delete pk;
+}
+int zkmi_pk_info(const zkmi_pk* pk, uint64_t out[3]) {
+  out[0] = pk->n;
+  out[1] = pk->num_instance;
+  out[2] = pk->num_witness;
+  return 0;
+}
+int zkmi_pk_vk_bytes(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {
+  *len = pk->vk_compressed.size();
+  if (buf && cap >= *len) memcpy(buf, pk->vk_compressed.data(), *len);
+  return 0;
+}
+int zkmi_groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const uint64_t* z, const uint64_t r[4],
+                       const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]) {
+  if (!ctx || !pk || !cs || !z || !r || !s) {
+    set_error("zkmi_groth16_prove: null argument");
+    return ZKMI_EINVAL;
+  }
+  int rc = groth16_prove(ctx, pk, cs, z, r, s, a_out, b_out, c_out);
+  if (rc == 0) rc = timer_flush(ctx);
+  return rc;
+}
+}  // extern "C"

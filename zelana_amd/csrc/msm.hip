@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <chrono>
 
+#include "dev_io.h"
 #include "ec.h"
 #include "zkmi_internal.h"
 
@@ -49,18 +50,6 @@ struct G2T {
   static constexpr int PW = 32;
 };
 
-__device__ __forceinline__ Fe ld_fe(const uint32_t* p) {
-  uint4 a = reinterpret_cast<const uint4*>(p)[0];
-  uint4 b = reinterpret_cast<const uint4*>(p)[1];
-  uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  return unpack(w);
-}
-__device__ __forceinline__ void st_fe(uint32_t* p, const Fe& f) {
-  uint32_t w[8];
-  pack(w, f);
-  reinterpret_cast<uint4*>(p)[0] = make_uint4(w[0], w[1], w[2], w[3]);
-  reinterpret_cast<uint4*>(p)[1] = make_uint4(w[4], w[5], w[6], w[7]);
-}
 template <class F>
 struct Io;
 template <>

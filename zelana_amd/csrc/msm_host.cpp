@@ -114,6 +114,63 @@ void host_g2_add_affine(const uint64_t a[16], const uint64_t b[16], uint64_t out
   to_affine<HFq2, 16>(r, out);
 }
 
+// ------------------------------------------------- Groth16 assembly (a4)
+template <class F, int K>
+static HX<F> smul(const uint64_t* aff, const uint64_t k[4]) {
+  HX<F> base = from_aff_canon<F, K>(aff), acc = xyzz_inf<F>();
+  for (int b = 255; b >= 0; b--) {
+    acc = xyzz_dbl(acc);
+    if ((k[b / 64] >> (b % 64)) & 1) acc = xyzz_add(acc, base);
+  }
+  return acc;
+}
+template <class F, int K>
+static HX<F> pt(const uint64_t* aff) {
+  return from_aff_canon<F, K>(aff);
+}
+static bool is_zero4(const uint64_t k[4]) { return (k[0] | k[1] | k[2] | k[3]) == 0; }
+
+void groth16_assemble(const uint64_t alpha_g1[8], const uint64_t beta_g1[8], const uint64_t delta_g1[8],
+                      const uint64_t beta_g2[16], const uint64_t delta_g2[16], const uint64_t a0[8],
+                      const uint64_t b1_0[8], const uint64_t b2_0[16], const uint64_t h_acc[8],
+                      const uint64_t l_acc[8], const uint64_t a_acc[8], const uint64_t b1_acc[8],
+                      const uint64_t b2_acc[16], const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8],
+                      uint64_t b_out[16], uint64_t c_out[8]) {
+  // A = r delta + a_query[0] + sum z a + alpha          (calculate_coeff)
+  HX<HFq> A = smul<HFq, 4>(delta_g1, r);
+  A = xyzz_add(A, pt<HFq, 4>(a0));
+  A = xyzz_add(A, pt<HFq, 4>(a_acc));
+  A = xyzz_add(A, pt<HFq, 4>(alpha_g1));
+  // B (G2) = s delta + b_g2_query[0] + sum z b + beta
+  HX<HFq2> B = smul<HFq2, 8>(delta_g2, s);
+  B = xyzz_add(B, pt<HFq2, 8>(b2_0));
+  B = xyzz_add(B, pt<HFq2, 8>(b2_acc));
+  B = xyzz_add(B, pt<HFq2, 8>(beta_g2));
+  // B (G1), only when r != 0 (as ark-groth16)
+  HX<HFq> B1 = xyzz_inf<HFq>();
+  if (!is_zero4(r)) {
+    B1 = smul<HFq, 4>(delta_g1, s);
+    B1 = xyzz_add(B1, pt<HFq, 4>(b1_0));
+    B1 = xyzz_add(B1, pt<HFq, 4>(b1_acc));
+    B1 = xyzz_add(B1, pt<HFq, 4>(beta_g1));
+  }
+  uint64_t Aaff[8], B1aff[8], sdelta[8];
+  to_affine<HFq, 8>(A, Aaff);
+  to_affine<HFq, 8>(B1, B1aff);
+  // C = s A + r B1 - r (s delta) + l + h
+  HX<HFq> C = smul<HFq, 4>(Aaff, s);
+  C = xyzz_add(C, smul<HFq, 4>(B1aff, r));
+  to_affine<HFq, 8>(smul<HFq, 4>(delta_g1, s), sdelta);
+  HX<HFq> rsd = smul<HFq, 4>(sdelta, r);
+  rsd.y = HFq::neg(rsd.y);
+  C = xyzz_add(C, rsd);
+  C = xyzz_add(C, pt<HFq, 4>(l_acc));
+  C = xyzz_add(C, pt<HFq, 4>(h_acc));
+  memcpy(a_out, Aaff, 64);
+  to_affine<HFq2, 16>(B, b_out);
+  to_affine<HFq, 8>(C, c_out);
+}
+
 // ---------------------------------------------------------- encodings
 static void put_le(uint8_t* o, const uint64_t c[4]) {
   for (int i = 0; i < 32; i++) o[i] = (uint8_t)(c[i / 8] >> (8 * (i % 8)));

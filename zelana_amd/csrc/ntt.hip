@@ -18,7 +18,7 @@
 
 #include <algorithm>
 
-#include "ff.h"
+#include "dev_io.h"
 #include "zkmi_internal.h"
 
 namespace zk {
@@ -30,24 +30,6 @@ __constant__ uint32_t W28I[8] = {0x9d18157eu, 0x72394277u, 0xfd399d5du, 0xec9d51
 __constant__ uint32_t GINV[8] = {0xc6666667u, 0xe7f3fbd4u, 0xca4a2d06u, 0xa9ae5ce9u,
                                  0x33cd568bu, 0x49b9b57cu, 0x5a13d9aau, 0x135b5294u};
 
-__device__ __forceinline__ Fe ldg_fe(const uint32_t* p) {
-  uint4 a = reinterpret_cast<const uint4*>(p)[0];
-  uint4 b = reinterpret_cast<const uint4*>(p)[1];
-  uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  return unpack(w);
-}
-__device__ __forceinline__ void stg_fe(uint32_t* p, const Fe& f) {
-  uint32_t w[8];
-  pack(w, f);
-  reinterpret_cast<uint4*>(p)[0] = make_uint4(w[0], w[1], w[2], w[3]);
-  reinterpret_cast<uint4*>(p)[1] = make_uint4(w[4], w[5], w[6], w[7]);
-}
-__device__ __forceinline__ Fe ldc_fe(const uint32_t* c) {
-  uint32_t w[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) w[i] = c[i];
-  return unpack(w);
-}
 __device__ __forceinline__ Fe mont_from_canon(const uint32_t* c) { return to_mont<FrP>(ldc_fe(c)); }
 
 // root of unity of order 2^logn (Montgomery), inverse if inv
@@ -74,7 +56,7 @@ __global__ void __launch_bounds__(256) k_ntt_twiddles(uint32_t* __restrict__ tw,
   Fe w = root_of_unity(logn, inv != 0);
   Fe cur = fe_pow_u64(w, e0);
   for (int k = 0; k < 64 && e0 + k < half; k++) {
-    stg_fe(tw + (e0 + k) * 8, reduce<FrP>(cur));
+    st_fe(tw + (e0 + k) * 8, reduce<FrP>(cur));
     cur = mul<FrP>(cur, w);
   }
 }
@@ -97,7 +79,7 @@ __global__ void __launch_bounds__(256) k_ntt_group(uint32_t* __restrict__ data, 
     uint64_t q = q0 + s;
     uint64_t col = q & ((1ull << colbits) - 1), blk = q >> colbits;
     uint64_t idx = (blk << a) + col + ((uint64_t)j << colbits);
-    Fe v = ldg_fe(data + idx * 8);
+    Fe v = ld_fe(data + idx * 8);
 #pragma unroll
     for (int l = 0; l < NL; l++) lds[e * NL + l] = v.v[l];
   }
@@ -123,7 +105,7 @@ __global__ void __launch_bounds__(256) k_ntt_group(uint32_t* __restrict__ data, 
       uint64_t i = (blk << a) + col + ((uint64_t)j0 << colbits);
       uint64_t jm = i & ((1ull << (logm - 1)) - 1);
       uint64_t te = jm << (logn - logm);
-      Fe w = ldg_fe(tw + te * 8);
+      Fe w = ld_fe(tw + te * 8);
       Fe x, y;
       if (DIT) {
         Fe t = mul<FrP>(v, w);
@@ -149,7 +131,7 @@ __global__ void __launch_bounds__(256) k_ntt_group(uint32_t* __restrict__ data, 
     Fe v;
 #pragma unroll
     for (int l = 0; l < NL; l++) v.v[l] = lds[e * NL + l];
-    stg_fe(data + idx * 8, v);
+    st_fe(data + idx * 8, v);
   }
 }
 
@@ -160,7 +142,7 @@ __global__ void __launch_bounds__(256) k_ntt_small(uint32_t* __restrict__ data, 
   extern __shared__ __align__(16) uint32_t lds[];
   const uint32_t n = 1u << logn;
   for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
-    Fe v = ldg_fe(data + (size_t)e * 8);
+    Fe v = ld_fe(data + (size_t)e * 8);
 #pragma unroll
     for (int l = 0; l < NL; l++) lds[e * NL + l] = v.v[l];
   }
@@ -177,7 +159,7 @@ __global__ void __launch_bounds__(256) k_ntt_small(uint32_t* __restrict__ data, 
         v.v[l] = lds[i1 * NL + l];
       }
       uint32_t te = (i0 & (h - 1)) << (logn - logm);
-      Fe w = ldg_fe(tw + (size_t)te * 8);
+      Fe w = ld_fe(tw + (size_t)te * 8);
       Fe x, y;
       if (DIT) {
         Fe t = mul<FrP>(v, w);
@@ -199,7 +181,7 @@ __global__ void __launch_bounds__(256) k_ntt_small(uint32_t* __restrict__ data, 
     Fe v;
 #pragma unroll
     for (int l = 0; l < NL; l++) v.v[l] = lds[e * NL + l];
-    stg_fe(data + (size_t)e * 8, v);
+    st_fe(data + (size_t)e * 8, v);
   }
 }
 
@@ -242,7 +224,7 @@ __global__ void __launch_bounds__(256) k_bitrev_tiled(uint32_t* __restrict__ dat
       for (int l = 0; l < 8; l++) w[l] = src[l];
       Fe v = reduce<FrP>(unpack(w));
       uint64_t oidx = ((uint64_t)rlo << (logn - b)) | ((uint64_t)omid << b) | rhi;
-      stg_fe(data + oidx * 8, v);
+      st_fe(data + oidx * 8, v);
     }
   }
 }
@@ -251,7 +233,7 @@ __global__ void __launch_bounds__(256) k_bitrev_naive(const uint32_t* __restrict
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (1u << logn)) return;
   uint32_t r = logn ? brev_bits(i, logn) : 0;
-  stg_fe(out + (size_t)r * 8, reduce<FrP>(ldg_fe(in + (size_t)i * 8)));
+  st_fe(out + (size_t)r * 8, reduce<FrP>(ld_fe(in + (size_t)i * 8)));
 }
 
 // data[i] = reduce(data[i] * c * g^(+-i)) in natural order; g^i by runs of 64.
@@ -276,7 +258,7 @@ __global__ void __launch_bounds__(256) k_ntt_scale(uint32_t* __restrict__ data, 
   }
   for (int k = 0; k < 64 && i0 + k < n; k++) {
     uint32_t* p = data + (i0 + k) * 8;
-    stg_fe(p, reduce<FrP>(mul<FrP>(ldg_fe(p), cur)));
+    st_fe(p, reduce<FrP>(mul<FrP>(ld_fe(p), cur)));
     if (mode & 2) cur = mul<FrP>(cur, g);
   }
 }

@@ -176,3 +176,94 @@ def g2_add(a, b):
     check(lib().zkmi_g2_add(_p64(np.ascontiguousarray(a, np.uint64)), _p64(np.ascontiguousarray(b, np.uint64)),
                             _p64(out)))
     return out
+
+
+def r1cs_struct(cs):
+    """zelana_amd.r1cs.R1CS -> (ctypes R1CSStruct, keep-alive list)."""
+    keep = []
+    s = R1CSStruct()
+    s.num_constraints, s.num_instance, s.num_witness = cs.num_constraints, cs.num_instance, cs.num_witness
+    for name in ("a", "b", "c"):
+        rp, col, val = cs.csr(name)
+        keep += [rp, col, val]
+        setattr(s, name + "_rowptr", rp.ctypes.data)
+        setattr(s, name + "_col", col.ctypes.data)
+        setattr(s, name + "_val", val.ctypes.data)
+    return s, keep
+
+
+class ProvingKey:
+    """arkworks ProvingKey<Bn254> resident on the GPU (zkmi_pk_load)."""
+
+    def __init__(self, ctx: Context, pk_bytes: bytes, compressed: bool = True):
+        self.ctx = ctx
+        self.h = vp()
+        buf = np.frombuffer(pk_bytes, np.uint8).copy()
+        check(lib().zkmi_pk_load(ctx.h, buf.ctypes.data_as(u8p), len(pk_bytes), int(compressed),
+                                 ctypes.byref(self.h)), "zkmi_pk_load")
+        info = np.zeros(3, np.uint64)
+        check(lib().zkmi_pk_info(self.h, _p64(info)))
+        self.n, self.num_instance, self.num_witness = (int(x) for x in info)
+
+    def vk_bytes(self) -> bytes:
+        ln = ctypes.c_size_t()
+        check(lib().zkmi_pk_vk_bytes(self.h, None, 0, ctypes.byref(ln)))
+        buf = np.zeros(ln.value, np.uint8)
+        check(lib().zkmi_pk_vk_bytes(self.h, buf.ctypes.data_as(u8p), ln.value, ctypes.byref(ln)))
+        return buf.tobytes()
+
+    def close(self):
+        if self.h:
+            lib().zkmi_pk_destroy(self.h)
+            self.h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _limbs(x: int) -> np.ndarray:
+    return np.array([(x >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], np.uint64)
+
+
+def groth16_prove(ctx: Context, pk: ProvingKey, cs, z: np.ndarray, r: int, s: int):
+    """Canonical affine (A[8], B[16], C[8]) as numpy u64."""
+    st, keep = r1cs_struct(cs)
+    z = np.ascontiguousarray(z, np.uint64).reshape(-1, 4)
+    a, b, c = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+    rr, ss = _limbs(r), _limbs(s)
+    check(lib().zkmi_groth16_prove(ctx.h, pk.h, ctypes.byref(st), _p64(z), _p64(rr), _p64(ss), _p64(a), _p64(b),
+                                   _p64(c)), "zkmi_groth16_prove")
+    del keep
+    return a, b, c
+
+
+def witness_map(ctx: Context, cs, z: np.ndarray) -> np.ndarray:
+    st, keep = r1cs_struct(cs)
+    z = np.ascontiguousarray(z, np.uint64).reshape(-1, 4)
+    m, l = cs.num_constraints, cs.num_instance
+    n = 1
+    while n < m + l:
+        n <<= 1
+    h = np.zeros((n, 4), np.uint64)
+    check(lib().zkmi_witness_map(ctx.h, ctypes.byref(st), _p64(z), _p64(h)), "zkmi_witness_map")
+    del keep
+    return h
+
+
+def proof_to_solana_bytes(a, b, c) -> bytes:
+    out = np.zeros(256, np.uint8)
+    check(lib().zkmi_proof_to_solana_bytes(_p64(np.ascontiguousarray(a, np.uint64)),
+                                           _p64(np.ascontiguousarray(b, np.uint64)),
+                                           _p64(np.ascontiguousarray(c, np.uint64)), out.ctypes.data_as(u8p)))
+    return out.tobytes()
+
+
+def proof_serialize_compressed(a, b, c) -> bytes:
+    out = np.zeros(128, np.uint8)
+    check(lib().zkmi_proof_serialize_compressed(_p64(np.ascontiguousarray(a, np.uint64)),
+                                                _p64(np.ascontiguousarray(b, np.uint64)),
+                                                _p64(np.ascontiguousarray(c, np.uint64)), out.ctypes.data_as(u8p)))
+    return out.tobytes()

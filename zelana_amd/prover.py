@@ -1,0 +1,166 @@
+"""Host-side mirror of the reference's prover plugin interface
+(core/src/sequencer/settlement/prover.rs):
+
+    trait BatchProver { prove(&inputs, &witness) -> Result<BatchProof>;
+                        verify(&proof) -> Result<bool>;
+                        verification_key_hash() -> [u8; 32] }       (:160-169)
+
+`Groth16Prover` keeps the same names, argument meaning and error behaviour
+(errors raise, the Rust `anyhow::Error` analogue) but every field/curve/
+polynomial operation runs in libzkmi.so on the MI355X:
+  from_bytes / from_files     (:263-286)  -> zkmi_pk_load (GPU decompression)
+  prove                       (:350-425)  -> StdRng::seed_from_u64(batch_id),
+                                              r, s = Fr::rand x2, zkmi_groth16_prove
+  proof_to_solana_bytes       (:304-334)  -> 256 B (-A || B || C, LE coordinates)
+  compute_vk_hash             (:289-294)  -> blake3(compressed vk)
+Circuit synthesis (L2BlockCircuit, prover/src/l2_circuit.rs) is pluggable: a
+`circuit` callable maps (inputs, witness) to (R1CS, full assignment z).
+"""
+from __future__ import annotations
+
+import base64
+import json
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import gpu
+from .blake3 import blake3
+from .rng import StdRng
+
+
+@dataclass
+class BatchPublicInputs:
+    """prover.rs BatchPublicInputs: 6 roots/hashes + batch_id."""
+    pre_state_root: bytes = bytes(32)
+    post_state_root: bytes = bytes(32)
+    pre_shielded_root: bytes = bytes(32)
+    post_shielded_root: bytes = bytes(32)
+    withdrawal_root: bytes = bytes(32)
+    batch_hash: bytes = bytes(32)
+    batch_id: int = 0
+
+
+@dataclass
+class BatchProof:
+    public_inputs: BatchPublicInputs
+    proof_bytes: bytes
+    proving_time_ms: int
+    # extra (not in the Rust struct): the arkworks points, for JSON export
+    a: np.ndarray | None = field(default=None, repr=False)
+    b: np.ndarray | None = field(default=None, repr=False)
+    c: np.ndarray | None = field(default=None, repr=False)
+
+
+class Groth16Prover:
+    """Drop-in for the reference Groth16Prover on one MI355X (one per process)."""
+
+    def __init__(self, ctx: gpu.Context, pk: gpu.ProvingKey, vk_bytes: bytes, circuit=None):
+        self.ctx = ctx
+        self.pk = pk
+        self.verifying_key = vk_bytes
+        self.vk_hash = blake3(vk_bytes)
+        self.circuit = circuit
+
+    @classmethod
+    def from_bytes(cls, pk_bytes: bytes, vk_bytes: bytes, device: int = 0, circuit=None, compressed=True):
+        """ProvingKey/VerifyingKey::deserialize_compressed (validated) -> resident pk."""
+        ctx = gpu.Context(device)
+        pk = gpu.ProvingKey(ctx, pk_bytes, compressed)
+        if vk_bytes != pk.vk_bytes():
+            raise ValueError("Failed to deserialize verifying key: does not match the proving key's")
+        return cls(ctx, pk, vk_bytes, circuit)
+
+    @classmethod
+    def from_files(cls, pk_path: str, vk_path: str, **kw):
+        with open(pk_path, "rb") as f:
+            pkb = f.read()
+        with open(vk_path, "rb") as f:
+            vkb = f.read()
+        return cls.from_bytes(pkb, vkb, **kw)
+
+    # ---------------------------------------------------------- BatchProver
+    def prove(self, inputs: BatchPublicInputs, witness) -> BatchProof:
+        if self.circuit is None:
+            raise NotImplementedError("no circuit synthesizer configured (L2BlockCircuit R1CS is SURVEY §8f next)")
+        cs, z = self.circuit(inputs, witness)
+        return self.prove_r1cs(cs, z, inputs)
+
+    def prove_r1cs(self, cs, z, inputs: BatchPublicInputs) -> BatchProof:
+        start = time.perf_counter()
+        rng = StdRng.seed_from_u64(inputs.batch_id)
+        r = rng.fr_rand()
+        s = rng.fr_rand()
+        a, b, c = gpu.groth16_prove(self.ctx, self.pk, cs, _as_z(z), r, s)
+        return BatchProof(inputs, self.proof_to_solana_bytes(a, b, c),
+                          int((time.perf_counter() - start) * 1000), a, b, c)
+
+    def verify(self, proof: BatchProof) -> bool:
+        # reference semantics (prover.rs:427-442): length check only
+        return len(proof.proof_bytes) == 256
+
+    def verification_key_hash(self) -> bytes:
+        return self.vk_hash
+
+    # ---------------------------------------------------------- encodings
+    @staticmethod
+    def proof_to_solana_bytes(a, b, c) -> bytes:
+        return gpu.proof_to_solana_bytes(a, b, c)
+
+    @staticmethod
+    def export_proof_json(proof: BatchProof) -> str:
+        """prover/src/snarkjs.rs:44-52 (l2_proof.json): base64 of the 128-B
+        compressed arkworks Proof."""
+        raw = gpu.proof_serialize_compressed(proof.a, proof.b, proof.c)
+        return json.dumps({"proof": base64.b64encode(raw).decode()}, indent=2)
+
+    def export_vk_json(self) -> str:
+        return json.dumps({"verifying_key": base64.b64encode(self.verifying_key).decode()}, indent=2)
+
+
+def _as_z(z):
+    if isinstance(z, np.ndarray):
+        return z
+    return np.array([[(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)] for v in z], np.uint64)
+
+
+def smoke_square_circuit(ctx: gpu.Context):
+    """Used by __graft_entry__.smoke(): SquareCircuit proof with pk from the
+    oracle setup must reproduce the reference's proof_for_onchain.json."""
+    import ctypes
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import oracle_ctypes as O
+
+    from .r1cs import square_circuit
+
+    cs, z = square_circuit(7)
+    st, keep = O.make_r1cs(cs)
+    rng = O.Rng(42)
+    opk = O.lib().oracle_groth16_setup(ctypes.byref(st), rng.h, 1)
+    buf = np.zeros(1 << 16, np.uint8)
+    nb = O.lib().oracle_pk_serialize(opk, 1, buf.ctypes.data, buf.size)
+    pk = gpu.ProvingKey(ctx, buf[:nb].tobytes(), True)
+    # the proof continues the setup's rng (snarkjs.rs:153-159): r then s
+    rs = np.zeros(8, np.uint64)
+    O.lib().oracle_fr_rand(rng.h, O.P(rs[:4]))
+    O.lib().oracle_fr_rand(rng.h, O.P(rs[4:]))
+    a, b, c = gpu.groth16_prove(ctx, pk, cs, _as_z(z), O.limbs_to_int(rs[:4]), O.limbs_to_int(rs[4:]))
+    with open(os.path.join(root, "tests", "golden", "ref_proof_for_onchain.json")) as f:
+        ref = json.load(f)["proof_components"]
+    ba = np.zeros(64, np.uint8)
+    O.lib().oracle_g1_serialize(O.P(a), 0, O.P(ba))
+    assert list(ba) == ref["pi_a"], "GPU proof pi_a != reference fixture"
+    bb = np.zeros(128, np.uint8)
+    O.lib().oracle_g2_serialize(O.P(b), 0, O.P(bb))
+    assert list(bb) == ref["pi_b"], "GPU proof pi_b != reference fixture"
+    bc = np.zeros(64, np.uint8)
+    O.lib().oracle_g1_serialize(O.P(c), 0, O.P(bc))
+    assert list(bc) == ref["pi_c"], "GPU proof pi_c != reference fixture"
+    O.lib().oracle_pk_free(opk)
+    pk.close()
+    del keep
