@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-ntt", action="store_true", help="skip the NTT 2^24 side measurement")
     ap.add_argument("--ntt-log-n", type=int, default=24)
+    ap.add_argument("--no-l2", action="store_true", help="skip the L2 proof throughput side measurement")
+    ap.add_argument("--l2-log-n", type=int, default=22, help="Groth16 domain 2^k for the L2 proof measurement")
+    ap.add_argument("--l2-steps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -126,6 +129,8 @@ def main():
     extra = {"msm_stage_ms_per_step": breakdown}
     if rank == 0 and world == 1 and not args.no_ntt:
         extra["ntt"] = bench_ntt(ctx, args.ntt_log_n)
+    if rank == 0 and world == 1 and not args.no_l2:
+        extra["l2_proofs"] = bench_l2(ctx, args.l2_log_n, args.l2_steps)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(ctx, bases, scalars, n, result, args.cpu_threads)
@@ -208,6 +213,55 @@ def bench_ntt(ctx, log_n, steps=5):
         "frac_hbm": round(alg / dt / 1e9 / HBM_PEAK_GBS, 5),
         "stage_ms": stages,
         "note": "VALU-bound (8 x 2^23 x 3 Montgomery butterflies); algorithmic bytes = 64 B/elem/transform",
+    }
+
+
+def bench_l2(ctx, log_n, steps):
+    """Groth16 proofs/s at the config-4 scale (BASELINE.json configs[3]:
+    ~2^22-constraint L2 block proof): synthetic R1CS of 2^log_n - 8 rows
+    (3 terms per row in A and B, 1 in C; 8 instance variables = One + 7
+    public inputs; one witness per row), random proving key of that shape
+    generated in HBM, witness resident in HBM.  One step = witness map
+    (3 mat-vecs, 7 NTTs) + 4 G1 MSMs + 1 G2 MSM + assembly."""
+    from zelana_amd import gpu
+    from zelana_amd.r1cs import synthetic_fast
+
+    l = 8
+    m = (1 << log_n) - l
+    w = m
+    t0 = time.perf_counter()
+    cs, z = synthetic_fast(m, l, w, seed=70)
+    pk = gpu.synthetic_pk(ctx, 70, log_n, l, w)
+    dev = gpu.R1CSDevice(ctx, cs)
+    dz = gpu.DeviceBuffer(ctx, z.nbytes)
+    dz.upload(z)
+    setup_s = time.perf_counter() - t0
+    gpu.groth16_prove_resident(ctx, pk, dev, dz, 12345, 67890)
+    ctx.sync()
+    ctx.profile(True)
+    ctx.profile_reset()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        gpu.groth16_prove_resident(ctx, pk, dev, dz, 12345 + i, 67890 + i)
+    ctx.sync()
+    dt = (time.perf_counter() - t0) / steps
+    ctx.profile(False)
+    stages = {}
+    for k in ("g16_matvec", "g16_scale", "g16_qap", "ntt_group", "ntt_small", "msm_sort", "msm_acc0_g1",
+              "msm_acc0_g2", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"):
+        t, c = ctx.profile_get(k)
+        if c:
+            stages[k] = round(t / steps, 3)
+    nnz = int(sum(cs.csr(k)[0][-1] for k in ("a", "b", "c")))
+    del dev, pk
+    return {
+        "workload": f"Groth16 prove, domain 2^{log_n}: {m} constraints, {l} instance + {w} witness vars, {nnz} non-zeros "
+                    "(BASELINE.json configs[3] scale; synthetic R1CS + random pk generated in HBM)",
+        "proofs_per_s": round(1.0 / dt, 3),
+        "ms_per_proof": round(dt * 1e3, 2),
+        "stage_ms_per_proof": stages,
+        "setup_s": round(setup_s, 1),
+        "note": "witness z resident in HBM; uploading it costs z_bytes/PCIe extra (see DESIGN.md)",
     }
 
 

@@ -52,6 +52,7 @@ typedef struct zkmi_ctx zkmi_ctx;
 typedef struct zkmi_bases zkmi_bases;
 typedef struct zkmi_pk zkmi_pk;
 typedef struct zkmi_msm_job zkmi_msm_job;
+typedef struct zkmi_r1cs_dev zkmi_r1cs_dev;
 
 const char* zkmi_last_error(void);
 int zkmi_version(void);
@@ -152,6 +153,21 @@ int zkmi_pk_vk_bytes(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len);
 int zkmi_groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const uint64_t* z,
                        const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
                        uint64_t c_out[8]);
+
+/* Circuit matrices resident in HBM: a proving key fits exactly one circuit
+ * shape (keygen.rs proves dummy()'s shape), so the
+ * matrices are uploaded once and only the witness changes per proof. */
+int zkmi_r1cs_create(zkmi_ctx* ctx, const zkmi_r1cs* cs, zkmi_r1cs_dev** out);
+void zkmi_r1cs_destroy(zkmi_r1cs_dev* cs);
+/* prove with R1CS and assignment z (n_vars x 32 B canonical) already in HBM */
+int zkmi_groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs_dev* cs, const void* d_z,
+                                const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
+                                uint64_t c_out[8]);
+/* Benchmark helper: a random proving key of domain 2^log_n with the given
+ * instance/witness counts, generated in HBM.  Proofs made with it do not
+ * verify; the proving work is identical to a real key of that shape. */
+int zkmi_pk_synthetic(zkmi_ctx* ctx, uint64_t seed, uint32_t log_n, size_t num_instance, size_t num_witness,
+                      zkmi_pk** out);
 
 /* ------------------------------------------------------------- encodings */
 /* 256 B Solana layout: -A (x,y LE) || B (x.c0,x.c1,y.c0,y.c1 LE) || C (x,y LE)

@@ -136,3 +136,37 @@ def test_pk_load_rejects_bad_points(ctx):
     with pytest.raises(ZkmiError):
         gpu.ProvingKey(ctx, bytes(bad), True)
     O.lib().oracle_pk_free(opk)
+
+
+def test_resident_prove_matches_host_prove(ctx):
+    """R1CS uploaded once (zkmi_r1cs_create) + witness in HBM gives the same
+    proof as the host-argument entry point, and the oracle's."""
+    from zelana_amd import gpu
+    from zelana_amd.r1cs import synthetic_fast
+    cs, z = synthetic_fast(1500, 4, 1600, seed=3)
+    opk, pkb, rng, (st, keep) = _setup(cs, 11)
+    pk = gpu.ProvingKey(ctx, pkb, True)
+    r, s = rng.fr(), rng.fr()
+    dev = gpu.R1CSDevice(ctx, cs)
+    dz = gpu.DeviceBuffer(ctx, z.nbytes)
+    dz.upload(z)
+    got = gpu.groth16_prove_resident(ctx, pk, dev, dz, r, s)
+    want = _oracle_prove(opk, st, z, r, s)
+    for g, wv in zip(got, want):
+        assert np.array_equal(g, wv)
+    again = gpu.groth16_prove(ctx, pk, cs, z, r, s)
+    for g, wv in zip(again, want):
+        assert np.array_equal(g, wv)
+    O.lib().oracle_pk_free(opk)
+
+
+def test_synthetic_pk_shape(ctx):
+    from zelana_amd import gpu
+    from zelana_amd.r1cs import synthetic_fast
+    cs, z = synthetic_fast(1000, 8, 1010, seed=4)
+    pk = gpu.synthetic_pk(ctx, 5, 10, 8, 1010)  # m + l = 1008 -> domain 2^10
+    dev = gpu.R1CSDevice(ctx, cs)
+    dz = gpu.DeviceBuffer(ctx, z.nbytes)
+    dz.upload(z)
+    a, b, c = gpu.groth16_prove_resident(ctx, pk, dev, dz, 3, 4)
+    assert O.lib().oracle_g1_on_curve(O.P(a)) and O.lib().oracle_g2_on_curve(O.P(b)) and O.lib().oracle_g1_on_curve(O.P(c))

@@ -364,11 +364,36 @@ static int domain_cache(zkmi_ctx* ctx, uint32_t logn, DomainCache* dc) {
   return 0;
 }
 
-struct DevR1CS {
-  uint64_t *rp[3], *col[3];
-  uint32_t* val[3];
+}  // namespace zk
+
+// R1CS matrices resident in HBM (the circuit shape is fixed per proving key,
+// Appendix B.1, so only the witness changes between proofs)
+struct zkmi_r1cs_dev {
+  size_t m = 0, l = 0, w = 0;
+  uint64_t* rp[3] = {nullptr, nullptr, nullptr};
+  uint64_t* col[3] = {nullptr, nullptr, nullptr};
+  uint32_t* val[3] = {nullptr, nullptr, nullptr};
+  bool owned = false;
+  ~zkmi_r1cs_dev() {
+    if (!owned) return;
+    for (int t = 0; t < 3; t++) {
+      hipFree(rp[t]);
+      hipFree(col[t]);
+      hipFree(val[t]);
+    }
+  }
 };
-static int upload_r1cs(zkmi_ctx* ctx, const zkmi_r1cs* cs, DevR1CS* d) {
+
+namespace zk {
+using DevR1CS = zkmi_r1cs_dev;
+
+// validate + copy a host CSR R1CS to device; owned=true allocates dedicated
+// buffers (zkmi_r1cs_create), otherwise context workspace is used
+static int upload_r1cs(zkmi_ctx* ctx, const zkmi_r1cs* cs, DevR1CS* d, bool owned = false) {
+  d->m = cs->num_constraints;
+  d->l = cs->num_instance;
+  d->w = cs->num_witness;
+  d->owned = owned;
   const uint64_t* rps[3] = {cs->a_rowptr, cs->b_rowptr, cs->c_rowptr};
   const uint64_t* cols[3] = {cs->a_col, cs->b_col, cs->c_col};
   const uint64_t* vals[3] = {cs->a_val, cs->b_val, cs->c_val};
@@ -392,13 +417,23 @@ static int upload_r1cs(zkmi_ctx* ctx, const zkmi_r1cs* cs, DevR1CS* d) {
         return ZKMI_EINVAL;
       }
     }
-    char b1[32], b2[32], b3[32];
-    snprintf(b1, 32, "r1cs_rp_%s", nm[t]);
-    snprintf(b2, 32, "r1cs_col_%s", nm[t]);
-    snprintf(b3, 32, "r1cs_val_%s", nm[t]);
-    ZK_TRY(ctx->ws.get(b1, (m + 1) * 8, (void**)&d->rp[t]));
-    ZK_TRY(ctx->ws.get(b2, std::max<uint64_t>(1, nnz) * 8, (void**)&d->col[t]));
-    ZK_TRY(ctx->ws.get(b3, std::max<uint64_t>(1, nnz) * 32, (void**)&d->val[t]));
+    if (owned) {
+      if (hipMalloc(&d->rp[t], (m + 1) * 8) != hipSuccess ||
+          hipMalloc(&d->col[t], std::max<uint64_t>(1, nnz) * 8) != hipSuccess ||
+          hipMalloc(&d->val[t], std::max<uint64_t>(1, nnz) * 32) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("r1cs: device allocation failed (matrix %s, %llu non-zeros)", nm[t], (unsigned long long)nnz);
+        return ZKMI_ENOMEM;
+      }
+    } else {
+      char b1[32], b2[32], b3[32];
+      snprintf(b1, 32, "r1cs_rp_%s", nm[t]);
+      snprintf(b2, 32, "r1cs_col_%s", nm[t]);
+      snprintf(b3, 32, "r1cs_val_%s", nm[t]);
+      ZK_TRY(ctx->ws.get(b1, (m + 1) * 8, (void**)&d->rp[t]));
+      ZK_TRY(ctx->ws.get(b2, std::max<uint64_t>(1, nnz) * 8, (void**)&d->col[t]));
+      ZK_TRY(ctx->ws.get(b3, std::max<uint64_t>(1, nnz) * 32, (void**)&d->val[t]));
+    }
     ZK_HIP(hipMemcpyAsync(d->rp[t], rps[t], (m + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
     if (nnz) {
       ZK_HIP(hipMemcpyAsync(d->col[t], cols[t], nnz * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -415,12 +450,10 @@ static uint32_t domain_log(size_t need) {
 }
 
 // h (bit-reversed layout, canonical, n elements) into d_h from device z
-static int witness_map_dev(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint32_t* d_z, uint32_t logn, uint32_t* d_h) {
+static int witness_map_dev(zkmi_ctx* ctx, const DevR1CS& dr, const uint32_t* d_z, uint32_t logn, uint32_t* d_h) {
   hipStream_t st = ctx->stream;
-  size_t m = cs->num_constraints, l = cs->num_instance, nv = l + cs->num_witness;
+  size_t m = dr.m, l = dr.l, nv = l + dr.w;
   size_t n = (size_t)1 << logn;
-  DevR1CS dr;
-  ZK_TRY(upload_r1cs(ctx, cs, &dr));
   DomainCache dc;
   ZK_TRY(domain_cache(ctx, logn, &dc));
   uint32_t *zm, *b, *c;
@@ -483,7 +516,9 @@ int witness_map_host(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t* z, uint
   ZK_TRY(ctx->ws.get("g16_z", nv * 32, (void**)&dz));
   ZK_TRY(ctx->ws.get("g16_h", n * 32, (void**)&dh));
   ZK_HIP(hipMemcpyAsync(dz, z, nv * 32, hipMemcpyHostToDevice, ctx->stream));
-  ZK_TRY(witness_map_dev(ctx, cs, dz, logn, dh));
+  DevR1CS dr;
+  ZK_TRY(upload_r1cs(ctx, cs, &dr));
+  ZK_TRY(witness_map_dev(ctx, dr, dz, logn, dh));
   ZK_TRY(ntt_bitrev(ctx, dh, logn));  // natural order for the caller
   ZK_HIP(hipMemcpyAsync(h_out, dh, n * 32, hipMemcpyDeviceToHost, ctx->stream));
   ZK_HIP(hipStreamSynchronize(ctx->stream));
@@ -657,23 +692,22 @@ int pk_load(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, int compressed, zkm
 }
 
 // ------------------------------------------------------------ prove
-int groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const uint64_t* z, const uint64_t r[4],
-                  const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]) {
-  ZK_TRY(check_cs(cs));
-  size_t l = cs->num_instance, w = cs->num_witness, nv = l + w;
-  uint32_t logn = domain_log(cs->num_constraints + l);
+// core: R1CS and full assignment z already resident in HBM
+int groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
+                           const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
+                           uint64_t c_out[8]) {
+  size_t l = dr.l, w = dr.w, nv = l + w;
+  uint32_t logn = domain_log(dr.m + l);
   if (l != pk->num_instance || w != pk->num_witness || ((size_t)1 << logn) != pk->n) {
     set_error("prove: circuit shape (m %zu, l %zu, w %zu) does not match the proving key (n %llu, l %llu, w %llu)",
-              cs->num_constraints, l, w, (unsigned long long)pk->n, (unsigned long long)pk->num_instance,
+              dr.m, l, w, (unsigned long long)pk->n, (unsigned long long)pk->num_instance,
               (unsigned long long)pk->num_witness);
     return ZKMI_EINVAL;
   }
   size_t n = pk->n;
-  uint32_t *dz, *dh;
-  ZK_TRY(ctx->ws.get("g16_z", nv * 32, (void**)&dz));
+  uint32_t* dh;
   ZK_TRY(ctx->ws.get("g16_h", n * 32, (void**)&dh));
-  ZK_HIP(hipMemcpyAsync(dz, z, nv * 32, hipMemcpyHostToDevice, ctx->stream));
-  ZK_TRY(witness_map_dev(ctx, cs, dz, logn, dh));
+  ZK_TRY(witness_map_dev(ctx, dr, dz, logn, dh));
   // 5 MSMs back to back; each host epilogue overlaps the next one's kernels
   zkmi_msm_job* jobs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   uint64_t h_acc[8], l_acc[8], a_acc[8], b1_acc[8], b2_acc[16];
@@ -693,6 +727,71 @@ int groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const u
   if (rc) return rc;
   groth16_assemble(pk->alpha_g1, pk->beta_g1, pk->delta_g1, pk->beta_g2, pk->delta_g2, pk->a0, pk->b1_0, pk->b2_0,
                    h_acc, l_acc, a_acc, b1_acc, b2_acc, r, s, a_out, b_out, c_out);
+  return 0;
+}
+
+int groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const uint64_t* z, const uint64_t r[4],
+                  const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]) {
+  ZK_TRY(check_cs(cs));
+  size_t nv = cs->num_instance + cs->num_witness;
+  uint32_t* dz;
+  ZK_TRY(ctx->ws.get("g16_z", nv * 32, (void**)&dz));
+  ZK_HIP(hipMemcpyAsync(dz, z, nv * 32, hipMemcpyHostToDevice, ctx->stream));
+  DevR1CS dr;
+  ZK_TRY(upload_r1cs(ctx, cs, &dr));
+  return groth16_prove_resident(ctx, pk, dr, dz, r, s, a_out, b_out, c_out);
+}
+
+// ------------------------------------------------------------ synthetic pk
+// Random proving key of a given shape, generated in HBM (benchmarks only:
+// the proof it yields does not verify, the work is identical).
+int pk_synthetic(zkmi_ctx* ctx, uint64_t seed, uint32_t log_n, size_t l, size_t w, zkmi_pk** out) {
+  *out = nullptr;
+  size_t n = (size_t)1 << log_n, nv = l + w;
+  if (l < 1 || log_n > 28) {
+    set_error("pk_synthetic: bad shape");
+    return ZKMI_EINVAL;
+  }
+  zkmi_pk* pk = new zkmi_pk;
+  pk->ctx = ctx;
+  pk->n = n;
+  pk->log_n = log_n;
+  pk->num_instance = l;
+  pk->num_witness = w;
+  int rc = 0;
+  auto fail = [&](int code) {
+    zkmi_pk_destroy(pk);
+    return code;
+  };
+  if ((rc = bases_generate(ctx, 0, seed + 1, nv, &pk->a_query))) return fail(rc);
+  if ((rc = bases_generate(ctx, 0, seed + 2, nv, &pk->b_g1_query))) return fail(rc);
+  if ((rc = bases_generate(ctx, 1, seed + 3, nv, &pk->b_g2_query))) return fail(rc);
+  if ((rc = bases_generate(ctx, 0, seed + 4, n - 1, &pk->h_query_rev))) return fail(rc);
+  if ((rc = bases_generate(ctx, 0, seed + 5, w, &pk->l_query))) return fail(rc);
+  zkmi_bases* small1;
+  zkmi_bases* small2;
+  if ((rc = bases_generate(ctx, 0, seed + 6, 3 + l, &small1))) return fail(rc);
+  if ((rc = bases_generate(ctx, 1, seed + 7, 3, &small2))) return fail(rc);
+  std::vector<uint64_t> s1((3 + l) * 8), s2(3 * 16), t1(nv * 8), t2(nv * 16);
+  rc = bases_export(small1, s1.data());
+  if (!rc) rc = bases_export(small2, s2.data());
+  zkmi_bases_destroy(small1);
+  zkmi_bases_destroy(small2);
+  if (rc) return fail(rc);
+  memcpy(pk->alpha_g1, &s1[0], 64);
+  memcpy(pk->beta_g1, &s1[8], 64);
+  memcpy(pk->delta_g1, &s1[16], 64);
+  pk->gamma_abc.assign(s1.begin() + 24, s1.end());
+  memcpy(pk->beta_g2, &s2[0], 128);
+  memcpy(pk->gamma_g2, &s2[16], 128);
+  memcpy(pk->delta_g2, &s2[32], 128);
+  if ((rc = bases_export(pk->a_query, t1.data()))) return fail(rc);
+  memcpy(pk->a0, t1.data(), 64);
+  if ((rc = bases_export(pk->b_g1_query, t1.data()))) return fail(rc);
+  memcpy(pk->b1_0, t1.data(), 64);
+  if ((rc = bases_export(pk->b_g2_query, t2.data()))) return fail(rc);
+  memcpy(pk->b2_0, t2.data(), 128);
+  *out = pk;
   return 0;
 }
 
@@ -730,6 +829,38 @@ int zkmi_pk_vk_bytes(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {
   *len = pk->vk_compressed.size();
   if (buf && cap >= *len) memcpy(buf, pk->vk_compressed.data(), *len);
   return 0;
+}
+int zkmi_r1cs_create(zkmi_ctx* ctx, const zkmi_r1cs* cs, zkmi_r1cs_dev** out) {
+  if (!ctx || !cs || !out) {
+    set_error("zkmi_r1cs_create: null argument");
+    return ZKMI_EINVAL;
+  }
+  ZK_TRY(check_cs(cs));
+  zkmi_r1cs_dev* d = new zkmi_r1cs_dev;
+  int rc = upload_r1cs(ctx, cs, d, true);
+  if (rc == 0) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : ZKMI_EHIP;
+  if (rc) {
+    delete d;
+    return rc;
+  }
+  *out = d;
+  return 0;
+}
+void zkmi_r1cs_destroy(zkmi_r1cs_dev* d) { delete d; }
+int zkmi_groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs_dev* cs, const void* d_z,
+                                const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
+                                uint64_t c_out[8]) {
+  if (!ctx || !pk || !cs || !d_z || !r || !s) {
+    set_error("zkmi_groth16_prove_resident: null argument");
+    return ZKMI_EINVAL;
+  }
+  int rc = groth16_prove_resident(ctx, pk, *cs, (const uint32_t*)d_z, r, s, a_out, b_out, c_out);
+  if (rc == 0) rc = timer_flush(ctx);
+  return rc;
+}
+int zkmi_pk_synthetic(zkmi_ctx* ctx, uint64_t seed, uint32_t log_n, size_t num_instance, size_t num_witness,
+                      zkmi_pk** out) {
+  return pk_synthetic(ctx, seed, log_n, num_instance, num_witness, out);
 }
 int zkmi_groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const uint64_t* z, const uint64_t r[4],
                        const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]) {

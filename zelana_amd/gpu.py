@@ -267,3 +267,44 @@ def proof_serialize_compressed(a, b, c) -> bytes:
                                                 _p64(np.ascontiguousarray(b, np.uint64)),
                                                 _p64(np.ascontiguousarray(c, np.uint64)), out.ctypes.data_as(u8p)))
     return out.tobytes()
+
+
+class R1CSDevice:
+    """Circuit matrices resident in HBM (zkmi_r1cs_create)."""
+
+    def __init__(self, ctx: Context, cs):
+        self.ctx = ctx
+        st, keep = r1cs_struct(cs)
+        self.h = vp()
+        check(lib().zkmi_r1cs_create(ctx.h, ctypes.byref(st), ctypes.byref(self.h)), "zkmi_r1cs_create")
+        self.num_variables = cs.num_instance + cs.num_witness
+        del keep
+
+    def close(self):
+        if self.h:
+            lib().zkmi_r1cs_destroy(self.h)
+            self.h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def synthetic_pk(ctx: Context, seed: int, log_n: int, num_instance: int, num_witness: int) -> "ProvingKey":
+    """Random proving key of the given shape generated in HBM (benchmarks)."""
+    pk = ProvingKey.__new__(ProvingKey)
+    pk.ctx = ctx
+    pk.h = vp()
+    check(lib().zkmi_pk_synthetic(ctx.h, seed, log_n, num_instance, num_witness, ctypes.byref(pk.h)),
+          "zkmi_pk_synthetic")
+    pk.n, pk.num_instance, pk.num_witness = 1 << log_n, num_instance, num_witness
+    return pk
+
+
+def groth16_prove_resident(ctx: Context, pk: "ProvingKey", r1cs: R1CSDevice, dz: DeviceBuffer, r: int, s: int):
+    a, b, c = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+    check(lib().zkmi_groth16_prove_resident(ctx.h, pk.h, r1cs.h, dz.ptr, _p64(_limbs(r)), _p64(_limbs(s)), _p64(a),
+                                            _p64(b), _p64(c)), "zkmi_groth16_prove_resident")
+    return a, b, c

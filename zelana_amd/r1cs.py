@@ -31,6 +31,8 @@ class R1CS:
 
     @property
     def num_constraints(self) -> int:
+        if getattr(self, "_m", None) is not None:
+            return self._m
         return len(self.rows["a"])
 
     @property
@@ -122,3 +124,31 @@ def synthetic(num_constraints: int, num_instance: int, num_witness: int, seed: i
     cs.rows = {"a": rows_a, "b": rows_b, "c": rows_c}
     zarr = np.array([_limbs(v) for v in z], np.uint64)
     return cs, zarr
+
+
+def _rand_fr_array(rng, count):
+    """count uniform values in [0, 2^253) (< r) as (count, 4) u64 limbs."""
+    v = rng.integers(0, 2**63, size=(count, 4), dtype=np.uint64) * 2 + rng.integers(0, 2, size=(count, 4), dtype=np.uint64)
+    v[:, 3] &= np.uint64((1 << 61) - 1)
+    return v
+
+
+def synthetic_fast(num_constraints: int, num_instance: int, num_witness: int, seed: int = 1, terms: int = 3):
+    """Large random R1CS built directly as CSR arrays (vectorised; for
+    throughput measurements at 2^20+ constraints).  Each row has `terms`
+    random (variable, coefficient) entries in A and B and one in C; the
+    random witness does not satisfy it — exactly the unsatisfiable-witness
+    regime of the reference's real batches.  z[0] = 1."""
+    rng = np.random.default_rng(seed)
+    m, nv = num_constraints, num_instance + num_witness
+    cs = R1CS(num_instance, num_witness)
+    cs.rows = {"a": [], "b": [], "c": []}
+    for name, t in (("a", terms), ("b", terms), ("c", 1)):
+        rp = np.arange(0, (m + 1) * t, t, dtype=np.uint64)
+        col = rng.integers(0, nv, size=m * t, dtype=np.uint64)
+        val = _rand_fr_array(rng, m * t)
+        cs.set_csr(name, rp, col, val)
+    cs._m = m
+    z = _rand_fr_array(rng, nv)
+    z[0] = [1, 0, 0, 0]
+    return cs, z
