@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log-n", type=int, default=20, help="points per GPU = 2^log_n")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-table", action="store_true", help="headline without the fixed-base table")
+    ap.add_argument("--no-plain", action="store_true", help="skip the no-table side measurement")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-ntt", action="store_true", help="skip the NTT 2^24 side measurement")
     ap.add_argument("--ntt-log-n", type=int, default=24)
@@ -99,34 +101,58 @@ def main():
             pending = nxt
         return finish(pending)
 
-    run(args.warmup)
-    sync_all()
-    ctx.profile(True)
-    ctx.profile_reset()
-    sync_all()
-    t0 = time.perf_counter()
-    result = run(args.steps)
-    sync_all()
-    elapsed = time.perf_counter() - t0
-    ctx.profile(False)
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(k, warm):
+        run(warm)
+        sync_all()
+        ctx.profile(True)
+        ctx.profile_reset()
+        sync_all()
+        t0 = time.perf_counter()
+        res = run(k)
+        sync_all()
+        dt = time.perf_counter() - t0
+        ctx.profile(False)
+        if dist is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return res, dt
+
+    def stages(k):
+        out = {}
+        for name in ("msm_sort", "msm_acc0_g1", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"):
+            t, c = ctx.profile_get(name)
+            if c:
+                out[name] = round(t / k, 4)
+        return out
+
+    # plain Pippenger first (no table: every window recomputed, as arkworks does)
+    plain = None
+    if not args.no_plain:
+        psteps = max(1, args.steps // 2)
+        pres, pdt = timed(psteps, 1)
+        plain = {"value": round(n * world * psteps / pdt / 1e6, 2), "ms_per_step": round(pdt / psteps * 1e3, 4),
+                 "stage_ms_per_step": stages(psteps)}
+    table = None
+    if not args.no_table:
+        t0 = time.perf_counter()
+        info = bases.precompute()
+        table = {"window": info[1], "copies": info[2], "windows": info[3],
+                 "build_s": round(time.perf_counter() - t0, 3),
+                 "hbm_bytes": info[2] * n * 64}
+    result, elapsed = timed(args.steps, args.warmup)
+    if plain is not None:
+        plain["same_result"] = bool(np.array_equal(pres, result))
 
     kernel = "msm_acc0_g1"
     ktot, kcnt = ctx.profile_get(kernel)
-    breakdown = {}
-    for k in ("msm_sort", "msm_acc0_g1", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"):
-        t, c = ctx.profile_get(k)
-        if c:
-            breakdown[k] = round(t / args.steps, 4)
+    breakdown = stages(args.steps)
     kavg_s = ktot / max(kcnt, 1) / 1e3
     achieved = MSM_BYTES_PER_PAIR * n / kavg_s / 1e9 if kcnt else None
     pairs_total = n * world * args.steps
     value = pairs_total / elapsed / 1e6
 
-    extra = {"msm_stage_ms_per_step": breakdown}
+    extra = {"msm_stage_ms_per_step": breakdown, "fixed_base_table": table, "msm_plain_no_table": plain}
     if rank == 0 and world == 1 and not args.no_ntt:
         extra["ntt"] = bench_ntt(ctx, args.ntt_log_n)
     if rank == 0 and world == 1 and not args.no_l2:
@@ -152,7 +178,9 @@ def main():
         "config": {
             "workload": f"BN254 G1 MSM, 2^{args.log_n} random scalars/points per GPU (BASELINE.json configs[1]"
                         + (f", sharded across {world} GPUs: global MSM of {world}x2^{args.log_n} points" if world > 1 else "")
-                        + "); bases resident in HBM",
+                        + "); bases resident in HBM"
+                        + ("; fixed-base table built once per base set (as for a proving key), outside the timed region"
+                           if table else ""),
             "log_n_per_gpu": args.log_n,
             "parallelism": f"point-shard x{world} + RCCL all-gather of partials" if world > 1 else "single GPU",
             "field": "BN254 Fq, 9x29-bit limbs, Montgomery R=2^261",
@@ -236,22 +264,33 @@ def bench_l2(ctx, log_n, steps):
     dz = gpu.DeviceBuffer(ctx, z.nbytes)
     dz.upload(z)
     setup_s = time.perf_counter() - t0
-    gpu.groth16_prove_resident(ctx, pk, dev, dz, 12345, 67890)
-    ctx.sync()
-    ctx.profile(True)
-    ctx.profile_reset()
+
+    def timed():
+        gpu.groth16_prove_resident(ctx, pk, dev, dz, 12345, 67890)
+        ctx.sync()
+        ctx.profile(True)
+        ctx.profile_reset()
+        t0 = time.perf_counter()
+        outs = []
+        for i in range(steps):
+            outs.append(gpu.groth16_prove_resident(ctx, pk, dev, dz, 12345 + i, 67890 + i))
+        ctx.sync()
+        dt = (time.perf_counter() - t0) / steps
+        ctx.profile(False)
+        st = {}
+        for k in ("g16_matvec", "g16_scale", "g16_qap", "ntt_group", "ntt_small", "msm_sort", "msm_acc0_g1",
+                  "msm_acc0_g2", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"):
+            t, c = ctx.profile_get(k)
+            if c:
+                st[k] = round(t / steps, 3)
+        return dt, st, outs
+
+    plain_dt, plain_st, plain_out = timed()
     t0 = time.perf_counter()
-    for i in range(steps):
-        gpu.groth16_prove_resident(ctx, pk, dev, dz, 12345 + i, 67890 + i)
-    ctx.sync()
-    dt = (time.perf_counter() - t0) / steps
-    ctx.profile(False)
-    stages = {}
-    for k in ("g16_matvec", "g16_scale", "g16_qap", "ntt_group", "ntt_small", "msm_sort", "msm_acc0_g1",
-              "msm_acc0_g2", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"):
-        t, c = ctx.profile_get(k)
-        if c:
-            stages[k] = round(t / steps, 3)
+    pk.precompute()
+    table_s = time.perf_counter() - t0
+    dt, stages, outs = timed()
+    same = all(all(np.array_equal(x, y) for x, y in zip(o1, o2)) for o1, o2 in zip(outs, plain_out))
     nnz = int(sum(cs.csr(k)[0][-1] for k in ("a", "b", "c")))
     del dev, pk
     return {
@@ -260,6 +299,9 @@ def bench_l2(ctx, log_n, steps):
         "proofs_per_s": round(1.0 / dt, 3),
         "ms_per_proof": round(dt * 1e3, 2),
         "stage_ms_per_proof": stages,
+        "fixed_base_tables": {"build_s": round(table_s, 2), "same_proofs_as_plain": same},
+        "plain_no_table": {"proofs_per_s": round(1.0 / plain_dt, 3), "ms_per_proof": round(plain_dt * 1e3, 2),
+                           "stage_ms_per_proof": plain_st},
         "setup_s": round(setup_s, 1),
         "note": "witness z resident in HBM; uploading it costs z_bytes/PCIe extra (see DESIGN.md)",
     }

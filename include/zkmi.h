@@ -81,6 +81,18 @@ void zkmi_bases_destroy(zkmi_bases* b);
 size_t zkmi_bases_len(const zkmi_bases* b);
 /* canonical affine copy of a base set (n x 8 or n x 16 u64) */
 int zkmi_bases_export(const zkmi_bases* b, uint64_t* affine_out);
+/* Fixed-base table for a base set that is reused across MSMs (a proving
+ * key's queries).  Stores `factor` shifted copies 2^(c*Wp*j) * P_i (Wp =
+ * ceil(W(c)/factor)) in HBM; later MSMs on this set with window c (the
+ * default unless zkmi_msm_set_window pins another) run Wp windows of
+ * factor*n entries instead of W(c) windows of n entries: same additions,
+ * 1/factor of the bucket reduction.  c = 0 picks the window for len(b);
+ * factor = 0 means a full table (one window).  Results are unchanged.
+ * Memory: factor x the base set.  No counterpart in the reference
+ * (arkworks recomputes every window per proof). */
+int zkmi_bases_precompute(zkmi_bases* b, int c, int factor);
+/* [len, table window c (0 = none), copies, windows per copy] */
+int zkmi_bases_info(const zkmi_bases* b, uint64_t out[4]);
 /* Deterministic synthetic inputs generated directly in HBM (benchmarks):
  * bases P_i = k_i * G (k_i from a splitmix64 stream of seed), scalars uniform
  * in [0, r) by rejection.  d_scalars must hold n x 32 bytes. */
@@ -109,6 +121,9 @@ int zkmi_msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const voi
 int zkmi_msm_wait(zkmi_msm_job* job, uint64_t* out_affine);
 /* window size override for experiments (0 = automatic) */
 int zkmi_msm_set_window(zkmi_ctx* ctx, int c);
+/* Number of MSM lanes (streams with their own scratch) used round-robin by
+ * consecutive submissions so their latency-bound tails overlap; 1..8. */
+int zkmi_msm_set_lanes(zkmi_ctx* ctx, int lanes);
 
 /* canonical affine point arithmetic helpers (host; used to combine per-GPU
  * partial MSM results after an RCCL all-gather) */
@@ -144,6 +159,10 @@ void zkmi_pk_destroy(zkmi_pk* pk);
 /* [n_domain, num_instance, num_witness] */
 int zkmi_pk_info(const zkmi_pk* pk, uint64_t out[3]);
 /* arkworks-compressed VerifyingKey bytes embedded in the pk (for vk hash) */
+/* Fixed-base tables for all five queries (zkmi_bases_precompute, window
+ * picked per query length; factor 0 = full).  Proofs are unchanged; a full
+ * table costs ~15x the key's HBM footprint (2^22 domain: ~24 GB). */
+int zkmi_pk_precompute(zkmi_pk* pk, int factor);
 int zkmi_pk_vk_bytes(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len);
 
 /* Full proof.  z: full assignment (One, instance..., witness...), canonical.

@@ -112,6 +112,10 @@ def test_synthetic_prove_and_witness_map(ctx, m, l, w, sat):
     want = _oracle_prove(opk, st, z, r, s)
     for g, wv in zip(got, want):
         assert np.array_equal(g, wv)
+    # fixed-base tables on every query (full for small keys, partial otherwise)
+    pk.precompute(0 if m < 2500 else 3)
+    for g, wv in zip(gpu.groth16_prove(ctx, pk, cs, z, r, s), want):
+        assert np.array_equal(g, wv)
     n = 1
     while n < m + l:
         n <<= 1

@@ -170,3 +170,62 @@ def test_msm_pipelined(ctx):
     sc = np.zeros((n, 4), np.uint64)
     d.download(sc)
     assert np.array_equal(r1, O.msm_g1(b.export()[:n - 1000], sc[:n - 1000]))
+
+
+# ---------------------------------------------------------- fixed-base tables
+@pytest.mark.parametrize("c,factor", [(0, 0), (8, 0), (11, 3), (13, 2), (16, 0), (17, 0), (17, 4), (6, 1)])
+def test_msm_g1_table(ctx, c, factor):
+    """MSM over a precomputed fixed-base table equals the plain MSM (oracle),
+    for full and partial tables, offsets and infinity bases."""
+    n = 3000
+    pts = O.gen_points_g1(300 + c, n)
+    pts[17:20] = 0
+    pts[40] = pts[41]
+    b = ctx.bases_g1(pts)
+    info = b.precompute(c, factor)
+    assert info[0] == n and info[1] >= 4 and info[2] * info[3] >= -(-254 // info[1])
+    assert np.array_equal(b.export(), pts)  # copy 0 untouched
+    rng = np.random.default_rng(c * 10 + factor)
+    for kind in ("uniform", "witness", "edge"):
+        sc = _rand_scalars(rng, n, kind)
+        assert np.array_equal(ctx.msm(b, sc), O.msm_g1(pts, sc))
+    sc = _rand_scalars(rng, 700)
+    assert np.array_equal(ctx.msm(b, sc, offset=1234), O.msm_g1(pts[1234:1934], sc))
+    # a pinned window different from the table's falls back to the plain path
+    other = 9 if info[1] != 9 else 10
+    ctx.set_window(other)
+    try:
+        assert np.array_equal(ctx.msm(b, sc, offset=5), O.msm_g1(pts[5:705], sc))
+    finally:
+        ctx.set_window(0)
+
+
+@pytest.mark.parametrize("factor", [0, 2])
+def test_msm_g2_table(ctx, factor):
+    n = 1500
+    pts = O.gen_points_g2(4000 + factor, n)
+    pts[3] = 0
+    b = ctx.bases_g2(pts)
+    b.precompute(0, factor)
+    sc = _rand_scalars(np.random.default_rng(factor), n, "witness")
+    assert np.array_equal(ctx.msm(b, sc), O.msm_g2(pts, sc))
+    assert np.array_equal(ctx.msm(b, sc[:900], offset=600), O.msm_g2(pts[600:], sc[:900]))
+
+
+def test_msm_table_2pow16_and_pipelined(ctx):
+    n = 1 << 16
+    pts = O.gen_points_g1(1016, n)
+    sc = O.gen_scalars(16, n)
+    b = ctx.bases_g1(pts)
+    b.precompute()
+    want = O.msm_g1(pts, sc)
+    assert np.array_equal(ctx.msm(b, sc), want)
+    g = ctx.bases_generate(seed=11, n=20000)
+    d = ctx.scalars_generate(seed=12, n=20000)
+    plain = ctx.msm(g, d)
+    g.precompute(17, 0)
+    jobs = [ctx.msm_submit(g, d, 20000), ctx.msm_submit(g, d, 19000, 0)]
+    assert np.array_equal(ctx.msm_wait(jobs[0]), plain)
+    sc2 = np.zeros((20000, 4), np.uint64)
+    d.download(sc2)
+    assert np.array_equal(ctx.msm_wait(jobs[1]), O.msm_g1(g.export()[:19000], sc2[:19000]))

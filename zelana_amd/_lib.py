@@ -52,6 +52,8 @@ SIGNATURES = [
     ("zkmi_bases_destroy", None, [vp]),
     ("zkmi_bases_len", sz, [vp]),
     ("zkmi_bases_export", ctypes.c_int, [vp, u64p]),
+    ("zkmi_bases_precompute", ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
+    ("zkmi_bases_info", ctypes.c_int, [vp, u64p]),
     ("zkmi_bases_generate_g1", ctypes.c_int, [vp, ctypes.c_uint64, sz, ctypes.POINTER(vp)]),
     ("zkmi_bases_generate_g2", ctypes.c_int, [vp, ctypes.c_uint64, sz, ctypes.POINTER(vp)]),
     ("zkmi_scalars_generate", ctypes.c_int, [vp, ctypes.c_uint64, sz, vp]),
@@ -62,6 +64,7 @@ SIGNATURES = [
     ("zkmi_msm_submit", ctypes.c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp)]),
     ("zkmi_msm_wait", ctypes.c_int, [vp, u64p]),
     ("zkmi_msm_set_window", ctypes.c_int, [vp, ctypes.c_int]),
+    ("zkmi_msm_set_lanes", ctypes.c_int, [vp, ctypes.c_int]),
     ("zkmi_g1_add", ctypes.c_int, [u64p, u64p, u64p]),
     ("zkmi_g2_add", ctypes.c_int, [u64p, u64p, u64p]),
     ("zkmi_ntt", ctypes.c_int, [vp, u64p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
@@ -70,6 +73,7 @@ SIGNATURES = [
     ("zkmi_pk_load", ctypes.c_int, [vp, u8p, sz, ctypes.c_int, ctypes.POINTER(vp)]),
     ("zkmi_pk_destroy", None, [vp]),
     ("zkmi_pk_info", ctypes.c_int, [vp, u64p]),
+    ("zkmi_pk_precompute", ctypes.c_int, [vp, ctypes.c_int]),
     ("zkmi_pk_vk_bytes", ctypes.c_int, [vp, u8p, sz, ctypes.POINTER(sz)]),
     ("zkmi_groth16_prove", ctypes.c_int, [vp, vp, ctypes.POINTER(R1CSStruct), u64p, u64p, u64p, u64p, u64p, u64p]),
     ("zkmi_r1cs_create", ctypes.c_int, [vp, ctypes.POINTER(R1CSStruct), ctypes.POINTER(vp)]),

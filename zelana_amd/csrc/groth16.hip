@@ -825,6 +825,19 @@ int zkmi_pk_info(const zkmi_pk* pk, uint64_t out[3]) {
   out[2] = pk->num_witness;
   return 0;
 }
+int zkmi_pk_precompute(zkmi_pk* pk, int factor) {
+  if (!pk) {
+    zk::set_error("zkmi_pk_precompute: null key");
+    return ZKMI_EINVAL;
+  }
+  zkmi_bases* qs[5] = {pk->h_query_rev, pk->l_query, pk->a_query, pk->b_g1_query, pk->b_g2_query};
+  for (zkmi_bases* b : qs) {
+    if (!b || b->tc) continue;
+    int rc = zk::bases_precompute(b, zk::table_window(b->n), factor);
+    if (rc) return rc;
+  }
+  return 0;
+}
 int zkmi_pk_vk_bytes(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {
   *len = pk->vk_compressed.size();
   if (buf && cap >= *len) memcpy(buf, pk->vk_compressed.data(), *len);

@@ -125,12 +125,14 @@ __device__ __forceinline__ void scalar_digits(const uint32_t* __restrict__ scala
   }
 }
 
-// Signed digits of every scalar, once per MSM: digits[w * n + i] (int32,
-// 0 = nothing to add; bases at infinity get all-zero digits).
+// Signed digits of every scalar, once per MSM (int32, 0 = nothing to add;
+// bases at infinity get all-zero digits).  Window w = j*Wp + w' of the plain
+// recoding is digit w' of table copy j: digits[(w' * p + j) * n + i], so the
+// sort sees Wp windows of p*n entries (p = 1, Wp = W without a table).
 template <int C>
 __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars,
-                                                    const uint32_t* __restrict__ bases, int pw, size_t n,
-                                                    int32_t* __restrict__ digits) {
+                                                    const uint32_t* __restrict__ bases, int pw, size_t n, int p,
+                                                    int Wp, int32_t* __restrict__ digits) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   constexpr int W = msm_windows(C);
@@ -138,7 +140,14 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__
   scalar_digits<C>(scalars, i, d);
   const bool inf = bases[i * pw + pw - 1] >> 31;
 #pragma unroll
-  for (int w = 0; w < W; w++) digits[(size_t)w * n + i] = inf ? 0 : d[w];
+  for (int w = 0; w < W; w++) {
+    int j = w / Wp, wq = w - j * Wp;
+    digits[((size_t)wq * p + j) * n + i] = inf ? 0 : d[w];
+  }
+  for (int w = W; w < p * Wp; w++) {
+    int j = w / Wp, wq = w - j * Wp;
+    digits[((size_t)wq * p + j) * n + i] = 0;
+  }
 }
 
 // Two-level counting sort.  Workgroup (chunk, w) owns up to SORT_CH points of
@@ -284,28 +293,64 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t* __restrict__ bstar
   return lo;
 }
 
+// A run cut by chunk edges leaves k = t1 - t0 + 1 partials of bucket b: the
+// tail slot of chunk t0 and the head slots of chunks t0+1..t1 (t = chunk of
+// its first / last entry).  k_msm_cutsum (one thread per bucket) sums and
+// invalidates them for k <= ACC_KMAX, so uniform scalars (a few pieces per
+// bucket) finish in one shallow pass; heavier buckets keep valid partials for
+// the k_msm_accN cascade.  (Kept out of k_msm_acc0: a second inlined curve
+// addition there costs a wave of occupancy.)
+constexpr uint32_t ACC_KMAX = 12;
+
+template <class G>
+__global__ void __launch_bounds__(256) k_msm_cutsum(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t L,
+                                                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xvalid,
+                                                    const uint32_t* __restrict__ xpts,
+                                                    uint32_t* __restrict__ open_flag) {
+  using F = typename G::F;
+  constexpr int XW = 4 * G::CW;
+  uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= K) return;
+  const uint32_t lo = bstart[b], hi = bstart[b + 1];
+  if (hi - lo < 2) return;
+  const uint32_t t0 = lo / L, t1 = (hi - 1) / L;
+  if (t0 == t1) return;  // complete inside one chunk: already in buckets[b]
+  if (t1 - t0 + 1 > ACC_KMAX) {
+    atomicOr(open_flag, 1u);
+    return;
+  }
+  Xyzz<F> sum = ld_xyzz<G>(xpts + (size_t)(2 * t0 + 2) * XW);
+  xvalid[2 * t0 + 2] = 0;
+  for (uint32_t t = t0 + 1; t <= t1; t++) {
+    sum = xyzz_add(sum, ld_xyzz<G>(xpts + (size_t)(2 * t + 1) * XW));
+    xvalid[2 * t + 1] = 0;
+  }
+  st_xyzz<G>(buckets + (size_t)b * XW, sum);
+}
+
 template <class G>
 __global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bstart,
                                                   uint32_t K, uint32_t L, uint32_t nchunks,
-                                                  const uint32_t* __restrict__ bases, uint32_t* __restrict__ buckets,
+                                                  const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
+                                                  uint32_t* __restrict__ buckets,
                                                   uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                                                  uint32_t* __restrict__ xpts, uint32_t* __restrict__ open_flag) {
+                                                  uint32_t* __restrict__ xpts) {
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nchunks) return;
   const uint32_t M = bstart[K];
   uint32_t start = t * L;
+  if (t == 0) {
+    xkey[0] = start >= M ? K : bucket_of(bstart, K, start);
+    xvalid[0] = 0;
+  }
   if (start >= M) {
     // beyond the data: keep the partial list sorted with max-key placeholders
     xkey[2 * t + 1] = K;
     xvalid[2 * t + 1] = 0;
     xkey[2 * t + 2] = K;
     xvalid[2 * t + 2] = 0;
-    if (t == 0) {
-      xkey[0] = K;
-      xvalid[0] = 0;
-    }
     return;
   }
   uint32_t end = min(start + L, M);
@@ -335,26 +380,24 @@ __global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ s
       } while (next_b == p);  // skip empty buckets
     }
     uint32_t v = sval[p];
-    Aff<F> P = ld_aff<G>(bases, v & 0x7FFFFFFFu);
+    uint32_t idx = v & 0x7FFFFFFFu;
+    if (tskip) idx += (idx / tn) * tskip;  // entry j*n + i -> table row j*N + i
+    Aff<F> P = ld_aff<G>(bases, idx);
     if (v >> 31) P.y = F::neg(P.y);
     acc = xyzz_madd(acc, P);
   }
-  bool left_open = first_run && left_cut;
-  bool right_open = next_b > end;
-  if (left_open) {
-    xkey[2 * t + 1] = cur;
-    xvalid[2 * t + 1] = 1;
-    st_xyzz<G>(xpts + (size_t)(2 * t + 1) * XW, acc);
-    head_done = true;
-  } else if (right_open) {
-    xkey[2 * t + 2] = cur;
-    xvalid[2 * t + 2] = 1;
-    st_xyzz<G>(xpts + (size_t)(2 * t + 2) * XW, acc);
-    tail_done = true;
+  const bool left_open = first_run && left_cut;
+  const bool right_open = next_b > end;
+  if (left_open || right_open) {
+    const uint32_t slot = left_open ? 2 * t + 1 : 2 * t + 2;
+    xkey[slot] = cur;
+    xvalid[slot] = 1;
+    st_xyzz<G>(xpts + (size_t)slot * XW, acc);
+    if (left_open) head_done = true;
+    else tail_done = true;
   } else {
     st_xyzz<G>(buckets + (size_t)cur * XW, acc);
   }
-  if (left_open || right_open) atomicOr(open_flag, 1u);
   if (!head_done) {
     xkey[2 * t + 1] = first_key;
     xvalid[2 * t + 1] = 0;
@@ -362,10 +405,6 @@ __global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ s
   if (!tail_done) {
     xkey[2 * t + 2] = cur;
     xvalid[2 * t + 2] = 0;
-  }
-  if (t == 0) {
-    xkey[0] = first_key;
-    xvalid[0] = 0;
   }
 }
 
@@ -675,6 +714,62 @@ __global__ void __launch_bounds__(256) k_gen_bases(uint64_t seed, size_t n, uint
     st_fe(q + 24, reduce<FqP>(y.c1));
   }
 }
+// Fixed-base table: copy j of point i is 2^(shift) * copy (j-1), in affine
+// form (one inversion of ZZ*ZZZ per copy).  Built once per base set (pk load);
+// MSMs then trade W windows of n entries for Wp windows of p*n entries, which
+// removes (p-1)/p of the bucket-reduction and Horner work and lets c grow.
+template <class F>
+__device__ __forceinline__ typename F::T inv_any(const typename F::T& a);
+template <>
+__device__ __forceinline__ Fe inv_any<FqOps>(const Fe& a) {
+  return fq_inv(a);
+}
+template <>
+__device__ __forceinline__ Fe2 inv_any<Fq2Ops>(const Fe2& a) {
+  Fe nrm = add<FqP>(sqr<FqP>(a.c0), sqr<FqP>(a.c1));
+  Fe ni = fq_inv(nrm);
+  return Fe2{mul<FqP>(a.c0, ni), neg<FqP>(mul<FqP>(a.c1, ni))};
+}
+template <class G>
+__global__ void __launch_bounds__(256) k_bases_table(uint32_t* __restrict__ pts, size_t n, int shift, int p,
+                                                     uint32_t* __restrict__ bad) {
+  using F = typename G::F;
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool inf = pts[i * G::PW + G::PW - 1] >> 31;
+  Aff<F> q = ld_aff<G>(pts, (uint32_t)i);
+  for (int j = 1; j < p; j++) {
+    uint32_t* o = pts + ((size_t)j * n + i) * G::PW;
+    if (inf) {
+      for (int k = 0; k < G::PW; k++) o[k] = 0;
+      o[G::PW - 1] = 0x80000000u;
+      continue;
+    }
+    Xyzz<F> acc = xyzz_mdbl(q);
+    for (int k = 1; k < shift; k++) acc = xyzz_dbl(acc);
+    if (xyzz_is_inf(acc)) {  // impossible without 2-power torsion; refuse
+      atomicOr(bad, 1u);
+      return;
+    }
+    auto t = inv_any<F>(F::mul(acc.zz, acc.zzz));
+    q.x = F::mul(acc.x, F::mul(t, acc.zzz));
+    q.y = F::mul(acc.y, F::mul(t, acc.zz));
+    if constexpr (G::CW == 8) {
+      q.x = reduce<FqP>(q.x);
+      q.y = reduce<FqP>(q.y);
+      st_fe(o, q.x);
+      st_fe(o + 8, q.y);
+    } else {
+      q.x = {reduce<FqP>(q.x.c0), reduce<FqP>(q.x.c1)};
+      q.y = {reduce<FqP>(q.y.c0), reduce<FqP>(q.y.c1)};
+      st_fe(o, q.x.c0);
+      st_fe(o + 8, q.x.c1);
+      st_fe(o + 16, q.y.c0);
+      st_fe(o + 24, q.y.c1);
+    }
+  }
+}
+
 // internal -> canonical affine (export for checking)
 template <class G>
 __global__ void __launch_bounds__(256) k_bases_export(const uint32_t* __restrict__ in, size_t n,
@@ -778,6 +873,75 @@ int bases_upload(zkmi_ctx* ctx, int g2, const uint64_t* host_affine, size_t n, z
   return bases_from_device_canon(ctx, g2, d_tmp, n, out);
 }
 
+int bases_precompute(zkmi_bases* b, int c, int factor) {
+  if (c < 4 || c > 17) {
+    set_error("bases_precompute: window %d outside [4, 17]", c);
+    return ZKMI_EINVAL;
+  }
+  const int W = msm_windows(c);
+  if (factor <= 0 || factor > W) factor = W;
+  const int Wp = (W + factor - 1) / factor;
+  const int p = (W + Wp - 1) / Wp;  // no copy beyond the last window
+  if ((size_t)p * b->n >= (1ull << 31)) {
+    set_error("bases_precompute: %d x %zu table rows exceed the 2^31 index space", p, b->n);
+    return ZKMI_EINVAL;
+  }
+  zkmi_ctx* ctx = b->ctx;
+  const int pw = b->g2 ? 32 : 16;
+  const size_t row = std::max<size_t>(1, b->n) * pw * 4;
+  uint32_t* d_tab = nullptr;
+  if (hipMalloc(&d_tab, row * p) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("hipMalloc(%zu) failed for the fixed-base table", row * p);
+    return ZKMI_ENOMEM;
+  }
+  uint32_t* d_bad;
+  int rc = ctx->ws.get("bases_bad", 4, (void**)&d_bad);
+  if (rc) {
+    hipFree(d_tab);
+    return rc;
+  }
+  hipStream_t st = ctx->stream;
+  uint32_t bad = 0;
+  hipError_t e = hipMemsetAsync(d_bad, 0, 4, st);
+  if (e == hipSuccess && b->n) e = hipMemcpyAsync(d_tab, b->d_pts, b->n * pw * 4, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess && b->n && p > 1) {
+    unsigned grid = (unsigned)((b->n + 255) / 256);
+    if (b->g2) k_bases_table<G2T><<<grid, 256, 0, st>>>(d_tab, b->n, c * Wp, p, d_bad);
+    else k_bases_table<G1T><<<grid, 256, 0, st>>>(d_tab, b->n, c * Wp, p, d_bad);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess || bad) {
+    hipFree(d_tab);
+    if (e != hipSuccess) set_error("bases_precompute: %s", hipGetErrorString(e));
+    else set_error("bases_precompute: a base reached infinity under doubling (not in a prime-order group)");
+    return e != hipSuccess ? ZKMI_EHIP : ZKMI_EPOINT;
+  }
+  hipFree(b->d_pts);
+  b->d_pts = d_tab;
+  b->tc = c;
+  b->tp = p;
+  b->tw = Wp;
+  return 0;
+}
+
+// Window for a full table over N bases: one window of W(c)*N entries and 2^(c-1)
+// buckets; bucket reduction costs ~3 additions per bucket.
+int table_window(size_t N) {
+  int best = 8;
+  double cost = 1e300;
+  for (int c = 6; c <= 17; c++) {
+    double k = (double)msm_windows(c) * (double)N + 3.0 * (double)(1u << (c - 1));
+    if (k < cost) {
+      cost = k;
+      best = c;
+    }
+  }
+  return best;
+}
+
 // ------------------------------------------------------------- driver
 static int pick_window(size_t n) {
   if (n < (1u << 10)) return 8;
@@ -789,14 +953,15 @@ static int pick_window(size_t n) {
 }
 
 template <int C>
-static void launch_digits(hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw, size_t n, int32_t* dg) {
-  k_msm_digits<C><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(sc, bases, pw, n, dg);
+static void launch_digits(hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw, size_t n, int p, int Wp,
+                          int32_t* dg) {
+  k_msm_digits<C><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(sc, bases, pw, n, p, Wp, dg);
 }
-static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw, size_t n,
-                           int32_t* dg) {
+static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw, size_t n, int p,
+                           int Wp, int32_t* dg) {
   switch (c) {
 #define ZK_C(CC) \
-  case CC: launch_digits<CC>(st, sc, bases, pw, n, dg); break;
+  case CC: launch_digits<CC>(st, sc, bases, pw, n, p, Wp, dg); break;
     ZK_C(4) ZK_C(5) ZK_C(6) ZK_C(7) ZK_C(8) ZK_C(9) ZK_C(10) ZK_C(11) ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15)
     ZK_C(16) ZK_C(17)
 #undef ZK_C
@@ -823,48 +988,84 @@ struct zkmi_msm_job {
 
 namespace zk {
 
+// round-robin MSM lanes, created on first use
+static int get_lane(zkmi_ctx* ctx, MsmLane** out) {
+  int nl = std::max(1, ctx->msm_lanes);
+  int i = ctx->lane_next++ % nl;
+  while ((int)ctx->lanes.size() <= i) {
+    MsmLane* l = new MsmLane;
+    if (hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&l->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&l->consumed, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      delete l;
+      set_error("msm: cannot create a stream / events for an MSM lane");
+      return ZKMI_EHIP;
+    }
+    ctx->lanes.push_back(l);
+  }
+  *out = ctx->lanes[i];
+  return 0;
+}
+
 template <class G>
-static int msm_submit_t(zkmi_ctx* ctx, const uint32_t* d_bases, const uint32_t* d_scalars, size_t n,
+static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, const uint32_t* d_scalars, size_t n,
                         zkmi_msm_job** out_job) {
   constexpr int XW = 4 * G::CW;
-  hipStream_t st = ctx->stream;
-  int c = ctx->msm_window > 0 ? ctx->msm_window : pick_window(n);
-  int W = msm_windows(c);
+  MsmLane* lane = nullptr;
+  ZK_TRY(get_lane(ctx, &lane));
+  hipStream_t st = lane->st;
+  Workspace& ws = lane->ws;
+  const uint32_t* d_bases = tb->d_pts + offset * G::PW;
+  // a fixed-base table is used when the caller did not pin another window
+  const bool table = tb->tc > 0 && (ctx->msm_window == 0 || ctx->msm_window == tb->tc);
+  const int c = table ? tb->tc : (ctx->msm_window > 0 ? ctx->msm_window : pick_window(n));
+  const int p = table ? tb->tp : 1;
+  const int W = table ? tb->tw : msm_windows(c);  // windows actually run
+  const size_t ne = (size_t)p * n;                  // entries per window
   uint32_t B = 1u << (c - 1);
   uint32_t K = (uint32_t)W * B;
   int bb = c - 1, lb = (bb + 1) / 2, hb = bb - lb;
   zkmi_msm_job* job = new zkmi_msm_job{ctx, G::CW == 16, c, W, bb, nullptr, 0, nullptr, n == 0};
   *out_job = job;
   if (n == 0) return 0;
-  if (n >= (1u << 31) || (size_t)W * n >= (1ull << 32)) {
+  if (ne >= (1u << 31) || (size_t)W * ne >= (1ull << 32)) {
     set_error("MSM size %zu too large for one call", n);
     return ZKMI_EINVAL;
   }
-  uint32_t nchunk = (uint32_t)((n + SORT_CH - 1) / SORT_CH);
+  const uint32_t tn = (uint32_t)n, tskip = p > 1 ? (uint32_t)(tb->n - n) : 0u;
+  uint32_t nchunk = (uint32_t)((ne + SORT_CH - 1) / SORT_CH);
   uint32_t *counts, *bstart, *bsums, *sval, *buckets, *flags;
   int32_t* digits;
   uint32_t nb = (K + 1023) / 1024;
-  size_t Mmax = (size_t)W * n;
-  ZK_TRY(ctx->ws.get("msm_digits", Mmax * 4, (void**)&digits));
-  ZK_TRY(ctx->ws.get("msm_counts", (size_t)K * nchunk * 4, (void**)&counts));
-  ZK_TRY(ctx->ws.get("msm_bstart", (size_t)(K + 1) * 4, (void**)&bstart));
-  ZK_TRY(ctx->ws.get("msm_bsums", (size_t)nb * 4 + 16, (void**)&bsums));
-  ZK_TRY(ctx->ws.get("msm_sval", Mmax * 4, (void**)&sval));
-  ZK_TRY(ctx->ws.get("msm_buckets", (size_t)K * XW * 4, (void**)&buckets));
-  ZK_TRY(ctx->ws.get("msm_flags", 64 * 4, (void**)&flags));
+  size_t Mmax = (size_t)W * ne;
+  ZK_TRY(ws.get("msm_digits", Mmax * 4, (void**)&digits));
+  ZK_TRY(ws.get("msm_counts", (size_t)K * nchunk * 4, (void**)&counts));
+  ZK_TRY(ws.get("msm_bstart", (size_t)(K + 1) * 4, (void**)&bstart));
+  ZK_TRY(ws.get("msm_bsums", (size_t)nb * 4 + 16, (void**)&bsums));
+  ZK_TRY(ws.get("msm_sval", Mmax * 4, (void**)&sval));
+  ZK_TRY(ws.get("msm_buckets", (size_t)K * XW * 4, (void**)&buckets));
+  ZK_TRY(ws.get("msm_flags", 64 * 4, (void**)&flags));
+
+  // fork from the context stream (inputs ready); the context stream only
+  // waits for the digits pass, the one reader of the scalars
+  ZK_HIP(hipEventRecord(lane->fork, ctx->stream));
+  ZK_HIP(hipStreamWaitEvent(st, lane->fork, 0));
   ZK_HIP(hipMemsetAsync(flags, 0, 64 * 4, st));
   {
-    ScopedKernelTimer tm(ctx, "msm_sort");
-    ZK_TRY(dispatch_digits(c, st, d_scalars, d_bases, G::PW, n, digits));
+    ScopedKernelTimer tm(ctx, "msm_sort", st);
+    ZK_TRY(dispatch_digits(c, st, d_scalars, d_bases, G::PW, n, p, W, digits));
+    ZK_HIP(hipEventRecord(lane->consumed, st));
+    ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
     dim3 grid(nchunk, W);
     size_t lds = (B / 2) * 4;
-    k_sort_count<<<grid, SORT_THREADS, lds, st>>>(digits, n, B, nchunk, counts);
+    k_sort_count<<<grid, SORT_THREADS, lds, st>>>(digits, ne, B, nchunk, counts);
     k_sort_chunk_prefix<<<(K + 255) / 256, 256, 0, st>>>(counts, nchunk, B, K, bstart);
     // exclusive scan of per-bucket totals (in bstart) -> bucket starts; bstart[K] = M
     k_scan_blocks<<<nb, 256, 0, st>>>(bstart, K, bstart, bsums);
     k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, bstart + K);
     k_scan_add<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, bsums, nullptr);
-    k_sort_scatter<<<grid, SORT_THREADS, lds, st>>>(digits, n, B, nchunk, counts, bstart, sval);
+    k_sort_scatter<<<grid, SORT_THREADS, lds, st>>>(digits, ne, B, nchunk, counts, bstart, sval);
     ZK_HIP(hipGetLastError());
   }
   // level 0: fixed-size chunks of the sorted list (sized from the upper bound
@@ -873,23 +1074,23 @@ static int msm_submit_t(zkmi_ctx* ctx, const uint32_t* d_bases, const uint32_t* 
   uint32_t nch = (uint32_t)((Mmax + L - 1) / L);
   uint32_t *xkey, *xvalid, *xpts, *ykey, *yvalid, *ypts;
   size_t xl = 2 * (size_t)nch + 1;
-  ZK_TRY(ctx->ws.get("msm_xkey", xl * 4 + 64, (void**)&xkey));
-  ZK_TRY(ctx->ws.get("msm_xvalid", xl * 4 + 64, (void**)&xvalid));
-  ZK_TRY(ctx->ws.get("msm_xpts", (xl + 2) * XW * 4, (void**)&xpts));
-  ZK_TRY(ctx->ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
-  ZK_TRY(ctx->ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
-  ZK_TRY(ctx->ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
+  ZK_TRY(ws.get("msm_xkey", xl * 4 + 64, (void**)&xkey));
+  ZK_TRY(ws.get("msm_xvalid", xl * 4 + 64, (void**)&xvalid));
+  ZK_TRY(ws.get("msm_xpts", (xl + 2) * XW * 4, (void**)&xpts));
+  ZK_TRY(ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
+  ZK_TRY(ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
+  ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
   {
-    ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2");
-    k_msm_acc0<G><<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, buckets, xkey, xvalid, xpts,
-                                                     &flags[0]);
+    ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
+    k_msm_acc0<G><<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, tn, tskip, buckets, xkey, xvalid, xpts);
+    k_msm_cutsum<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, L, buckets, xvalid, xpts, &flags[0]);
     ZK_HIP(hipGetLastError());
   }
   // segmented reduction of cut runs: level 1 pairs (tail, head) halves,
   // deeper levels only carry heavy buckets; each level exits on device when
   // the previous one left nothing open (no host round-trips)
   {
-    ScopedKernelTimer tm(ctx, "msm_accN");
+    ScopedKernelTimer tm(ctx, "msm_accN", st);
     uint32_t cur_len = (uint32_t)xl;
     for (int level = 1; cur_len > 1; level++) {
       if (level >= 63) {
@@ -909,11 +1110,11 @@ static int msm_submit_t(zkmi_ctx* ctx, const uint32_t* d_bases, const uint32_t* 
   }
   // bucket reduction -> W*(bb+1) canonical bit sums
   uint32_t *Cb, *Db, *sums;
-  ZK_TRY(ctx->ws.get("msm_C", (size_t)W * (1u << hb) * XW * 4, (void**)&Cb));
-  ZK_TRY(ctx->ws.get("msm_D", (size_t)W * (1u << lb) * XW * 4, (void**)&Db));
-  ZK_TRY(ctx->ws.get("msm_sums", (size_t)W * (bb + 1) * XW * 4, (void**)&sums));
+  ZK_TRY(ws.get("msm_C", (size_t)W * (1u << hb) * XW * 4, (void**)&Cb));
+  ZK_TRY(ws.get("msm_D", (size_t)W * (1u << lb) * XW * 4, (void**)&Db));
+  ZK_TRY(ws.get("msm_sums", (size_t)W * (bb + 1) * XW * 4, (void**)&sums));
   {
-    ScopedKernelTimer tm(ctx, "msm_bucket_reduce");
+    ScopedKernelTimer tm(ctx, "msm_bucket_reduce", st);
     uint32_t jobs1 = (uint32_t)W * ((1u << hb) + (1u << lb)), jobs2 = (uint32_t)W * (bb + 1);
     k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, st>>>(buckets, nullptr, bstart, lb, hb, W, Cb, Db);
     k_msm_br<G, true><<<(jobs2 + 3) / 4, 256, 0, st>>>(Cb, Db, nullptr, lb, hb, W, sums, nullptr);
@@ -934,8 +1135,8 @@ int msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_
     set_error("msm: range [%zu, %zu) outside base set of %zu", offset, offset + n, b ? b->n : 0);
     return ZKMI_EINVAL;
   }
-  int rc = b->g2 ? msm_submit_t<G2T>(ctx, b->d_pts + offset * 32, (const uint32_t*)d_scalars, n, job)
-                 : msm_submit_t<G1T>(ctx, b->d_pts + offset * 16, (const uint32_t*)d_scalars, n, job);
+  int rc = b->g2 ? msm_submit_t<G2T>(ctx, b, offset, (const uint32_t*)d_scalars, n, job)
+                 : msm_submit_t<G1T>(ctx, b, offset, (const uint32_t*)d_scalars, n, job);
   if (rc != 0 && *job) {
     msm_job_free(*job);
     *job = nullptr;
@@ -968,7 +1169,7 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
     msm_job_free(job);
     return ZKMI_EHIP;
   }
-  int rc = timer_flush(ctx);
+  int rc = timer_flush(ctx, false);
   auto th0 = std::chrono::steady_clock::now();
   // terms: V_{c w + j} = U_{w,j} (j < c-1), then T_w at weight 2^{c w}
   int c = job->c, W = job->W, bb = job->bb, nbits = c * W;

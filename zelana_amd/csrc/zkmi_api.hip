@@ -52,26 +52,31 @@ void Workspace::release_all() {
   bufs.clear();
 }
 
-void timer_begin(zkmi_ctx* ctx, const char* name, hipEvent_t* ev) {
+void timer_begin(zkmi_ctx* ctx, const char* name, hipEvent_t* ev, hipStream_t st) {
   *ev = nullptr;
   if (!ctx->timer.enabled) return;
   if (hipEventCreate(ev) != hipSuccess) {
     *ev = nullptr;
     return;
   }
-  hipEventRecord(*ev, ctx->stream);
+  hipEventRecord(*ev, st);
 }
-void timer_end(zkmi_ctx* ctx, const char* name, hipEvent_t ev) {
+void timer_end(zkmi_ctx* ctx, const char* name, hipEvent_t ev, hipStream_t st) {
   if (!ctx->timer.enabled || !ev) return;
   hipEvent_t e2;
   if (hipEventCreate(&e2) != hipSuccess) return;
-  hipEventRecord(e2, ctx->stream);
+  hipEventRecord(e2, st);
   ctx->timer.pending.push_back({ev, e2, name});
 }
-int timer_flush(zkmi_ctx* ctx) {
+int timer_flush(zkmi_ctx* ctx, bool wait) {
   if (ctx->timer.pending.empty()) return 0;
-  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  std::vector<KernelTimer::Rec> keep;
   for (auto& r : ctx->timer.pending) {
+    if (!wait && hipEventQuery(r.b) != hipSuccess) {
+      keep.push_back(r);
+      continue;
+    }
+    ZK_HIP(hipEventSynchronize(r.b));
     float ms = 0;
     hipEventElapsedTime(&ms, r.a, r.b);
     auto& t = ctx->timer.totals[r.name];
@@ -80,7 +85,12 @@ int timer_flush(zkmi_ctx* ctx) {
     hipEventDestroy(r.a);
     hipEventDestroy(r.b);
   }
-  ctx->timer.pending.clear();
+  ctx->timer.pending.swap(keep);
+  return 0;
+}
+int ctx_sync_all(zkmi_ctx* ctx) {
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  for (auto* l : ctx->lanes) ZK_HIP(hipStreamSynchronize(l->st));
   return 0;
 }
 
@@ -154,9 +164,17 @@ int zkmi_ctx_create(int device, zkmi_ctx** out) {
 void zkmi_ctx_destroy(zkmi_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
+  ctx_sync_all(ctx);
   timer_flush(ctx);
   ctx->ws.release_all();
+  for (auto* l : ctx->lanes) {
+    l->ws.release_all();
+    hipEventDestroy(l->fork);
+    hipEventDestroy(l->consumed);
+    hipStreamDestroy(l->st);
+    delete l;
+  }
+  ctx->lanes.clear();
   for (auto& pb : ctx->pinned_free) hipHostFree(pb.first);
   ctx->pinned_free.clear();
   hipStreamDestroy(ctx->stream);
@@ -202,10 +220,7 @@ int zkmi_d2h(zkmi_ctx* ctx, void* dst, const void* src, size_t bytes) {
   ZK_HIP(hipStreamSynchronize(ctx->stream));
   return 0;
 }
-int zkmi_sync(zkmi_ctx* ctx) {
-  ZK_HIP(hipStreamSynchronize(ctx->stream));
-  return 0;
-}
+int zkmi_sync(zkmi_ctx* ctx) { return ctx_sync_all(ctx); }
 
 // ------------------------------------------------------------------ MSM
 int zkmi_bases_create_g1(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_bases** out) {
@@ -226,6 +241,28 @@ int zkmi_bases_export(const zkmi_bases* b, uint64_t* affine_out) {
     return ZKMI_EINVAL;
   }
   return bases_export(b, affine_out);
+}
+int zkmi_bases_precompute(zkmi_bases* b, int c, int factor) {
+  if (!b) {
+    set_error("zkmi_bases_precompute: null bases");
+    return ZKMI_EINVAL;
+  }
+  if (b->tc) {
+    set_error("zkmi_bases_precompute: base set already has a table (window %d)", b->tc);
+    return ZKMI_EINVAL;
+  }
+  return bases_precompute(b, c > 0 ? c : table_window(b->n), factor);
+}
+int zkmi_bases_info(const zkmi_bases* b, uint64_t out[4]) {
+  if (!b) {
+    set_error("zkmi_bases_info: null bases");
+    return ZKMI_EINVAL;
+  }
+  out[0] = b->n;
+  out[1] = (uint64_t)b->tc;
+  out[2] = (uint64_t)b->tp;
+  out[3] = (uint64_t)b->tw;
+  return 0;
 }
 int zkmi_bases_generate_g1(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** out) {
   return bases_generate(ctx, 0, seed, n, out);
@@ -281,6 +318,14 @@ int zkmi_msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const voi
   return msm_submit(ctx, b, offset, d_scalars, n, job);
 }
 int zkmi_msm_wait(zkmi_msm_job* job, uint64_t* out_affine) { return msm_wait(job, out_affine); }
+int zkmi_msm_set_lanes(zkmi_ctx* ctx, int lanes) {
+  if (!ctx || lanes < 1 || lanes > 8) {
+    set_error("zkmi_msm_set_lanes: lanes must be in [1, 8]");
+    return ZKMI_EINVAL;
+  }
+  ctx->msm_lanes = lanes;
+  return 0;
+}
 int zkmi_msm_set_window(zkmi_ctx* ctx, int c) {
   if (c != 0 && (c < 4 || c > 17)) {
     set_error("window %d outside [4, 17]", c);

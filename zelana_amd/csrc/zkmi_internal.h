@@ -37,6 +37,15 @@ struct Workspace {
   void release_all();
 };
 
+// An MSM lane: its own stream and scratch, so consecutive MSMs overlap (the
+// latency-bound tail of one -- segmented and bucket reduction -- runs beside
+// the sort / accumulation of the next).
+struct MsmLane {
+  hipStream_t st = nullptr;
+  Workspace ws;
+  hipEvent_t fork = nullptr, consumed = nullptr;
+};
+
 struct KernelTimer {
   bool enabled = false;
   struct Rec {
@@ -57,6 +66,9 @@ struct zkmi_ctx {
   zk::KernelTimer timer;
   int msm_window = 0;  // 0 = auto
   int num_cus = 256;
+  int msm_lanes = 2;  // concurrent MSM streams
+  int lane_next = 0;
+  std::vector<zk::MsmLane*> lanes;
 };
 
 struct zkmi_bases {
@@ -64,21 +76,33 @@ struct zkmi_bases {
   int g2;           // 0 = G1 (16 words / point), 1 = G2 (32 words / point)
   size_t n;
   uint32_t* d_pts;  // packed affine, internal Montgomery, inf flag = bit 31 of last word
+  // Fixed-base table (zkmi_bases_precompute): d_pts holds tp copies of the n
+  // points, copy j = 2^(tc * tw * j) * P_i, so an MSM with window tc runs tw
+  // windows of tp*n entries instead of tp*tw windows of n entries.
+  int tc = 0;  // table window (0 = no table: plain bases, any window)
+  int tp = 1;  // copies
+  int tw = 0;  // windows per copy
 };
 
 namespace zk {
 // kernel timing helpers (events on ctx->stream)
-void timer_begin(zkmi_ctx* ctx, const char* name, hipEvent_t* ev);
-void timer_end(zkmi_ctx* ctx, const char* name, hipEvent_t ev);
-int timer_flush(zkmi_ctx* ctx);
+void timer_begin(zkmi_ctx* ctx, const char* name, hipEvent_t* ev, hipStream_t st);
+void timer_end(zkmi_ctx* ctx, const char* name, hipEvent_t ev, hipStream_t st);
+// wait = false: collect only the records whose work has finished
+int timer_flush(zkmi_ctx* ctx, bool wait = true);
 
 struct ScopedKernelTimer {
   zkmi_ctx* ctx;
   const char* name;
+  hipStream_t st;
   hipEvent_t ev = nullptr;
-  ScopedKernelTimer(zkmi_ctx* c, const char* n) : ctx(c), name(n) { timer_begin(ctx, name, &ev); }
-  ~ScopedKernelTimer() { timer_end(ctx, name, ev); }
+  ScopedKernelTimer(zkmi_ctx* c, const char* n, hipStream_t s = nullptr) : ctx(c), name(n), st(s ? s : c->stream) {
+    timer_begin(ctx, name, &ev, st);
+  }
+  ~ScopedKernelTimer() { timer_end(ctx, name, ev, st); }
 };
+// synchronise the context stream and every MSM lane
+int ctx_sync_all(zkmi_ctx* ctx);
 
 // pinned host staging buffers (pooled per context)
 int ctx_pinned_get(zkmi_ctx* ctx, size_t bytes, void** out);
@@ -98,6 +122,8 @@ int bases_from_device_canon(zkmi_ctx* ctx, int g2, const uint32_t* d_canon, size
 // synthetic inputs generated in HBM (bench) and canonical export (checks)
 int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t n, zkmi_bases** out);
 int bases_export(const zkmi_bases* b, uint64_t* host_out);
+int bases_precompute(zkmi_bases* b, int c, int factor);
+int table_window(size_t N);
 int scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_out);
 
 // NTT entry (ntt.hip): in-place on device, natural order

@@ -60,6 +60,17 @@ class Bases:
         f = lib().zkmi_bases_create_g2 if g2 else lib().zkmi_bases_create_g1
         check(f(ctx.h, _p64(pts), self.n, ctypes.byref(self.h)), "zkmi_bases_create")
 
+    def precompute(self, c: int = 0, factor: int = 0):
+        """Build the fixed-base table (see zkmi_bases_precompute); returns info()."""
+        check(lib().zkmi_bases_precompute(self.h, c, factor), "zkmi_bases_precompute")
+        return self.info()
+
+    def info(self):
+        """(len, table window or 0, copies, windows per copy)"""
+        out = np.zeros(4, np.uint64)
+        check(lib().zkmi_bases_info(self.h, _p64(out)), "zkmi_bases_info")
+        return tuple(int(v) for v in out)
+
     def export(self):
         out = np.zeros((self.n, 16 if self.g2 else 8), np.uint64)
         check(lib().zkmi_bases_export(self.h, _p64(out)), "zkmi_bases_export")
@@ -104,6 +115,9 @@ class Context:
 
     def set_window(self, c: int):
         check(lib().zkmi_msm_set_window(self.h, c))
+
+    def set_lanes(self, lanes: int):
+        check(lib().zkmi_msm_set_lanes(self.h, lanes))
 
     def sync(self):
         check(lib().zkmi_sync(self.h))
@@ -204,6 +218,11 @@ class ProvingKey:
         info = np.zeros(3, np.uint64)
         check(lib().zkmi_pk_info(self.h, _p64(info)))
         self.n, self.num_instance, self.num_witness = (int(x) for x in info)
+
+    def precompute(self, factor: int = 0):
+        """Fixed-base tables for all queries (zkmi_pk_precompute); proofs unchanged."""
+        check(lib().zkmi_pk_precompute(self.h, factor), "zkmi_pk_precompute")
+        return self
 
     def vk_bytes(self) -> bytes:
         ln = ctypes.c_size_t()

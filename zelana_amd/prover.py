@@ -64,12 +64,18 @@ class Groth16Prover:
         self.circuit = circuit
 
     @classmethod
-    def from_bytes(cls, pk_bytes: bytes, vk_bytes: bytes, device: int = 0, circuit=None, compressed=True):
-        """ProvingKey/VerifyingKey::deserialize_compressed (validated) -> resident pk."""
+    def from_bytes(cls, pk_bytes: bytes, vk_bytes: bytes, device: int = 0, circuit=None, compressed=True,
+                   precompute: bool = True):
+        """ProvingKey/VerifyingKey::deserialize_compressed (validated) -> resident pk.
+
+        precompute: build fixed-base tables for the pk queries once here (HBM
+        cost ~15x the key) so every later prove runs one MSM window per query."""
         ctx = gpu.Context(device)
         pk = gpu.ProvingKey(ctx, pk_bytes, compressed)
         if vk_bytes != pk.vk_bytes():
             raise ValueError("Failed to deserialize verifying key: does not match the proving key's")
+        if precompute:
+            pk.precompute()
         return cls(ctx, pk, vk_bytes, circuit)
 
     @classmethod
