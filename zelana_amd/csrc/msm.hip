@@ -3,14 +3,13 @@
 // a7/a8), called by ark-groth16 for h/l/a/b_g1 (G1) and b_g2 (G2).
 //
 // Pipeline (one HIP stream, all intermediate data resident in HBM):
-//   1. k_sort_count   two-level counting sort, pass 1: workgroup (chunk of 64K
-//                     points, window) recomputes the signed c-bit digits and
-//                     counts them in an LDS histogram (packed u16, no global
-//                     atomics).  Bases at infinity are skipped.
-//   2. prefix/scan    per-(window,bucket) chunk prefixes + global bucket starts.
-//   3. k_sort_scatter pass 2: LDS atomic rank -> each (point, sign) lands in its
-//                     bucket's slot.  Order inside a bucket is irrelevant:
-//                     group addition is exact, so results are bit-identical.
+//   1. k_msm_digits   signed c-bit digits of every scalar (bases at infinity
+//                     get none); with a fixed-base table, window w of copy j.
+//   2. k_rs_*         two-pass MSD radix sort of (window, bucket) keys with
+//                     LDS-ranked scatters and device-wide scans for offsets.
+//   3.                bucket starts come out of the second pass's scan.  Order
+//                     inside a bucket is irrelevant: group addition is exact,
+//                     so results are bit-identical.
 //   4. k_msm_acc0     load balance by construction: every thread owns a fixed
 //                     chunk of L sorted entries (not a bucket), accumulating
 //                     affine points into an XYZZ register accumulator with
@@ -150,76 +149,243 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__
   }
 }
 
-// Two-level counting sort.  Workgroup (chunk, w) owns up to SORT_CH points of
-// window w and counts its digits in an LDS histogram of packed u16 counters
-// (2^(c-1) buckets -> 64 KB at c = 16, 128 KB at c = 17): no global atomics.
-constexpr uint32_t SORT_CH = 65535;  // < 2^16 so a u16 counter cannot overflow
-constexpr int SORT_THREADS = 1024;
+// Bucket sort of the (window, bucket) keys: two-pass MSD radix sort.
+//   key = w * B + |digit| - 1  (K = W * B <= 2^21 keys), value = i | sign<<31
+//   P1: hi = key >> 8 (NH <= 8192 bins).  Workgroup = chunk of C1 digits; LDS
+//       histogram -> count matrix [hi][chunk] -> one device-wide scan gives
+//       every (bin, chunk) its output offset; the scatter ranks with LDS
+//       atomics on those offsets, so each chunk writes runs of C1/NH entries.
+//   P2: lo = key & 255 inside every hi bin.  Tiles of <= C2 entries never
+//       cross a bin; count matrix laid out [hi][lo][tile] so the scan yields
+//       final positions and the bucket starts directly.
+// Only zero digits are dropped; order inside a bucket is irrelevant (group
+// addition is exact), so neither pass needs to be stable.
+constexpr int RS_THREADS = 256;
+constexpr uint32_t RS_LO = 8;
 
-__global__ void __launch_bounds__(SORT_THREADS) k_sort_count(const int32_t* __restrict__ digits, size_t n, uint32_t B,
-                                                             uint32_t nchunk, uint32_t* __restrict__ counts) {
-  extern __shared__ uint32_t hist[];  // B/2 words of two u16 counters
-  const uint32_t chunk = blockIdx.x, w = blockIdx.y;
-  for (uint32_t k = threadIdx.x; k < B / 2; k += SORT_THREADS) hist[k] = 0;
-  __syncthreads();
-  const int32_t* dg = digits + (size_t)w * n;
-  size_t lo = (size_t)chunk * SORT_CH, hi = lo + SORT_CH < n ? lo + SORT_CH : n;
-  for (size_t i = lo + threadIdx.x; i < hi; i += SORT_THREADS) {
-    int32_t d = dg[i];
-    if (d != 0) {
-      uint32_t idx = (uint32_t)(d < 0 ? -d : d) - 1;
-      atomicAdd(&hist[idx >> 1], 1u << ((idx & 1) * 16));
-    }
-  }
-  __syncthreads();
-  uint32_t* out = counts + ((size_t)w * nchunk + chunk) * B;
-  for (uint32_t b = threadIdx.x; b < B; b += SORT_THREADS) out[b] = (hist[b >> 1] >> ((b & 1) * 16)) & 0xFFFFu;
+__device__ __forceinline__ bool rs_key(const int32_t* __restrict__ digits, uint64_t e, uint32_t ne, uint32_t B,
+                                       uint32_t& key, uint32_t& val) {
+  int32_t d = digits[e];
+  if (d == 0) return false;
+  uint32_t w = (uint32_t)(e / ne), i = (uint32_t)(e - (uint64_t)w * ne);
+  key = w * B + (uint32_t)(d < 0 ? -d : d) - 1;
+  val = i | (d < 0 ? 0x80000000u : 0u);
+  return true;
 }
 
-// per (w, b): counts[w][c][b] -> exclusive prefix over c (in place); totals[w*B+b]
-__global__ void __launch_bounds__(256) k_sort_chunk_prefix(uint32_t* __restrict__ counts, uint32_t nchunk, uint32_t B,
-                                                           uint32_t K, uint32_t* __restrict__ totals) {
-  uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= K) return;
-  uint32_t w = k / B, b = k % B;
-  uint32_t run = 0;
-  for (uint32_t c = 0; c < nchunk; c++) {
-    uint32_t* p = counts + ((size_t)w * nchunk + c) * B + b;
-    uint32_t v = *p;
-    *p = run;
-    run += v;
-  }
-  totals[k] = run;
-}
-
-__global__ void __launch_bounds__(SORT_THREADS) k_sort_scatter(const int32_t* __restrict__ digits, size_t n, uint32_t B,
-                                                               uint32_t nchunk, const uint32_t* __restrict__ cprefix,
-                                                               const uint32_t* __restrict__ bstart,
-                                                               uint32_t* __restrict__ sval) {
+__global__ void __launch_bounds__(RS_THREADS) k_rs_p1_count(const int32_t* __restrict__ digits, uint64_t M, uint32_t ne,
+                                                            uint32_t B, uint32_t NH, uint32_t C1, uint32_t nc1,
+                                                            uint32_t* __restrict__ cnt1) {
   extern __shared__ uint32_t hist[];
-  const uint32_t chunk = blockIdx.x, w = blockIdx.y;
-  for (uint32_t k = threadIdx.x; k < B / 2; k += SORT_THREADS) hist[k] = 0;
+  for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) hist[x] = 0;
   __syncthreads();
-  const uint32_t* cp = cprefix + ((size_t)w * nchunk + chunk) * B;
-  const uint32_t* bs = bstart + (size_t)w * B;
-  const int32_t* dg = digits + (size_t)w * n;
-  size_t lo = (size_t)chunk * SORT_CH, hi = lo + SORT_CH < n ? lo + SORT_CH : n;
-  for (size_t i = lo + threadIdx.x; i < hi; i += SORT_THREADS) {
-    int32_t d = dg[i];
-    if (d != 0) {
-      uint32_t idx = (uint32_t)(d < 0 ? -d : d) - 1;
-      uint32_t sh = (idx & 1) * 16;
-      uint32_t old = atomicAdd(&hist[idx >> 1], 1u << sh);
-      uint32_t rank = (old >> sh) & 0xFFFFu;
-      sval[bs[idx] + cp[idx] + rank] = (uint32_t)i | (d < 0 ? 0x80000000u : 0u);
+  const uint64_t base = (uint64_t)blockIdx.x * C1;
+  for (uint32_t k = threadIdx.x; k < C1; k += RS_THREADS) {
+    uint64_t e = base + k;
+    uint32_t key, val;
+    if (e < M && rs_key(digits, e, ne, B, key, val)) atomicAdd(&hist[key >> RS_LO], 1u);
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) cnt1[(size_t)x * nc1 + blockIdx.x] = hist[x];
+}
+
+// Scatter through LDS: each sub-tile of RS_ST entries is first ordered by bin
+// in LDS (rank = LDS atomic, bin starts = block scan), then written out so
+// that consecutive lanes store consecutive addresses of one bin's run.
+// Without this the stores of a wave hit 64 different lines and partially
+// written lines get evicted (measured: ~10x slower than the reads).
+constexpr int RS_ST = 4096;
+constexpr int RS_PER = RS_ST / RS_THREADS;
+
+// exclusive block scan of a[0..nb) in place (nb <= 8192); returns nothing,
+// tmp has RS_THREADS words
+__device__ __forceinline__ void rs_block_scan(uint32_t* a, uint32_t nb, uint32_t* tmp) {
+  const uint32_t per = (nb + RS_THREADS - 1) / RS_THREADS, b0 = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < per; k++)
+    if (b0 + k < nb) sum += a[b0 + k];
+  tmp[threadIdx.x] = sum;
+  __syncthreads();
+  for (int off = 1; off < RS_THREADS; off <<= 1) {
+    uint32_t t = threadIdx.x >= (unsigned)off ? tmp[threadIdx.x - off] : 0;
+    __syncthreads();
+    tmp[threadIdx.x] += t;
+    __syncthreads();
+  }
+  uint32_t run = tmp[threadIdx.x] - sum;
+  for (uint32_t k = 0; k < per; k++) {
+    if (b0 + k < nb) {
+      uint32_t v = a[b0 + k];
+      a[b0 + k] = run;
+      run += v;
     }
   }
+  __syncthreads();
+}
+
+// LDS layout: hist[nb] | lstart[nb] | gbase[nb] | tmp[256] | skey[RS_ST] | sval[RS_ST]
+template <class Load, class Bin, bool WRITE_KEY>
+__device__ __forceinline__ void rs_scatter_tiles(uint32_t count, uint32_t nb, uint32_t* lds, Load load, Bin bin,
+                                                 uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+  uint32_t* hist = lds;
+  uint32_t* lstart = lds + nb;
+  uint32_t* gbase = lds + 2 * nb;
+  uint32_t* tmp = lds + 3 * nb;
+  uint32_t* skey = tmp + RS_THREADS;
+  uint32_t* sval = skey + RS_ST;
+  for (uint32_t s0 = 0; s0 < count; s0 += RS_ST) {
+    for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) hist[x] = 0;
+    __syncthreads();
+    uint32_t key[RS_PER], val[RS_PER], rk[RS_PER];
+    bool ok[RS_PER];
+#pragma unroll
+    for (int k = 0; k < RS_PER; k++) {
+      uint32_t e = s0 + k * RS_THREADS + threadIdx.x;
+      ok[k] = e < count && load(e, key[k], val[k]);
+      if (ok[k]) rk[k] = atomicAdd(&hist[bin(key[k])], 1u);
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) lstart[x] = hist[x];
+    __syncthreads();
+    rs_block_scan(lstart, nb, tmp);
+    uint32_t total = lstart[nb - 1] + hist[nb - 1];
+#pragma unroll
+    for (int k = 0; k < RS_PER; k++) {
+      if (ok[k]) {
+        uint32_t lp = lstart[bin(key[k])] + rk[k];
+        skey[lp] = key[k];
+        sval[lp] = val[k];
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < total; q += RS_THREADS) {
+      uint32_t kk = skey[q], bn = bin(kk);
+      uint32_t g = gbase[bn] + (q - lstart[bn]);
+      if (WRITE_KEY) okey[g] = kk;
+      oval[g] = sval[q];
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) gbase[x] += hist[x];
+    __syncthreads();
+  }
+}
+
+__host__ __device__ constexpr size_t rs_scatter_lds(uint32_t nb) { return (3 * (size_t)nb + RS_THREADS + 2 * RS_ST) * 4; }
+
+__global__ void __launch_bounds__(RS_THREADS) k_rs_p1_scatter(const int32_t* __restrict__ digits, uint64_t M,
+                                                              uint32_t ne, uint32_t B, uint32_t NH, uint32_t C1,
+                                                              uint32_t nc1, const uint32_t* __restrict__ offs1,
+                                                              uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+  extern __shared__ uint32_t lds[];
+  for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) lds[2 * NH + x] = offs1[(size_t)x * nc1 + blockIdx.x];
+  const uint64_t base = (uint64_t)blockIdx.x * C1;
+  const uint32_t count = (uint32_t)std::min<uint64_t>(C1, M - base);
+  auto load = [&](uint32_t e, uint32_t& key, uint32_t& val) { return rs_key(digits, base + e, ne, B, key, val); };
+  auto bin = [](uint32_t key) { return key >> RS_LO; };
+  rs_scatter_tiles<decltype(load), decltype(bin), true>(count, NH, lds, load, bin, okey, oval);
+}
+
+// one workgroup: bin starts and tile starts (tiles of <= C2 entries per bin)
+__global__ void __launch_bounds__(1024) k_rs_tiles(const uint32_t* __restrict__ offs1, uint32_t nc1, uint32_t NH,
+                                                   const uint32_t* __restrict__ total, uint32_t C2,
+                                                   uint32_t* __restrict__ binstart, uint32_t* __restrict__ tstart) {
+  __shared__ uint32_t sh[1024];
+  const uint32_t tot = *total;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < NH; base += 1024) {
+    uint32_t h = base + threadIdx.x;
+    uint32_t nt = 0;
+    if (h < NH) {
+      uint32_t lo = offs1[(size_t)h * nc1], hi = h + 1 < NH ? offs1[(size_t)(h + 1) * nc1] : tot;
+      binstart[h] = lo;
+      nt = (hi - lo + C2 - 1) / C2;
+    }
+    sh[threadIdx.x] = nt;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      uint32_t t = threadIdx.x >= (unsigned)off ? sh[threadIdx.x - off] : 0;
+      __syncthreads();
+      sh[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (h < NH) tstart[h] = carry + sh[threadIdx.x] - nt;
+    uint32_t blk = sh[1023];
+    __syncthreads();
+    carry += blk;
+  }
+  if (threadIdx.x == 0) {
+    binstart[NH] = tot;
+    tstart[NH] = carry;
+  }
+}
+
+// tile t -> its bin h (largest h with tstart[h] <= t; bins without tiles skipped)
+__device__ __forceinline__ uint32_t rs_tile_bin(const uint32_t* __restrict__ tstart, uint32_t NH, uint32_t t) {
+  uint32_t lo = 0, hi = NH;  // tstart[lo] <= t < tstart[hi]
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (tstart[mid] <= t) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(RS_THREADS) k_rs_p2_count(const uint32_t* __restrict__ okey,
+                                                            const uint32_t* __restrict__ binstart,
+                                                            const uint32_t* __restrict__ tstart, uint32_t NH,
+                                                            uint32_t C2, uint32_t* __restrict__ cnt2) {
+  __shared__ uint32_t hist[1u << RS_LO];
+  const uint32_t t = blockIdx.x;
+  if (t >= tstart[NH]) return;
+  const uint32_t h = rs_tile_bin(tstart, NH, t), q = t - tstart[h], nt = tstart[h + 1] - tstart[h];
+  const uint32_t lo = binstart[h] + q * C2, hi = min(lo + C2, binstart[h + 1]);
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t p = lo + threadIdx.x; p < hi; p += RS_THREADS) atomicAdd(&hist[okey[p] & 255u], 1u);
+  __syncthreads();
+  cnt2[(size_t)tstart[h] * 256 + (size_t)threadIdx.x * nt + q] = hist[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(RS_THREADS) k_rs_p2_scatter(const uint32_t* __restrict__ okey,
+                                                              const uint32_t* __restrict__ oval,
+                                                              const uint32_t* __restrict__ binstart,
+                                                              const uint32_t* __restrict__ tstart, uint32_t NH,
+                                                              uint32_t C2, const uint32_t* __restrict__ offs2,
+                                                              uint32_t* __restrict__ sval) {
+  extern __shared__ uint32_t lds[];
+  const uint32_t t = blockIdx.x;
+  if (t >= tstart[NH]) return;
+  const uint32_t h = rs_tile_bin(tstart, NH, t), q = t - tstart[h], nt = tstart[h + 1] - tstart[h];
+  const uint32_t lo = binstart[h] + q * C2, hi = min(lo + C2, binstart[h + 1]);
+  lds[2 * 256 + threadIdx.x] = offs2[(size_t)tstart[h] * 256 + (size_t)threadIdx.x * nt + q];
+  auto load = [&](uint32_t e, uint32_t& key, uint32_t& val) {
+    key = okey[lo + e];
+    val = oval[lo + e];
+    return true;
+  };
+  auto bin = [](uint32_t key) { return key & 255u; };
+  rs_scatter_tiles<decltype(load), decltype(bin), false>(hi - lo, 256, lds, load, bin, nullptr, sval);
+}
+
+// bucket starts: start of key k = scanned count at (hi, lo, tile 0)
+__global__ void __launch_bounds__(256) k_rs_bstart(const uint32_t* __restrict__ offs2,
+                                                   const uint32_t* __restrict__ binstart,
+                                                   const uint32_t* __restrict__ tstart, uint32_t NH, uint32_t K,
+                                                   uint32_t* __restrict__ bstart) {
+  uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (k > K) return;
+  if (k == K) {
+    bstart[K] = binstart[NH];
+    return;
+  }
+  uint32_t h = k >> RS_LO, lo = k & 255u, nt = tstart[h + 1] - tstart[h];
+  bstart[k] = nt ? offs2[(size_t)tstart[h] * 256 + (size_t)lo * nt] : binstart[h];
 }
 
 // ----------------------------------------------------------------- scan
 // exclusive scan of counts[K] -> offs[K+1]; 1024 elements per block
-__global__ void __launch_bounds__(256) k_scan_blocks(const uint32_t* __restrict__ in, uint32_t K,
-                                                     uint32_t* __restrict__ out, uint32_t* __restrict__ block_sums) {
+__global__ void __launch_bounds__(256) k_scan_blocks(const uint32_t* in, uint32_t K, uint32_t* out,
+                                                     uint32_t* __restrict__ block_sums) {
   __shared__ uint32_t sh[256];
   uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
   uint32_t v[4], s = 0;
@@ -1034,16 +1200,28 @@ static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, cons
     return ZKMI_EINVAL;
   }
   const uint32_t tn = (uint32_t)n, tskip = p > 1 ? (uint32_t)(tb->n - n) : 0u;
-  uint32_t nchunk = (uint32_t)((ne + SORT_CH - 1) / SORT_CH);
-  uint32_t *counts, *bstart, *bsums, *sval, *buckets, *flags;
+  uint32_t *bstart, *sval, *buckets, *flags;
   int32_t* digits;
-  uint32_t nb = (K + 1023) / 1024;
   size_t Mmax = (size_t)W * ne;
+  // radix-sort geometry (see k_rs_*): ~2K P1 chunks, ~8K P2 tiles at most
+  const uint32_t NH = (K + 255) >> RS_LO;
+  const uint32_t C1 = 16384u * (uint32_t)std::max<size_t>(1, (Mmax + 16384ull * 2048 - 1) / (16384ull * 2048));
+  const uint32_t nc1 = (uint32_t)((Mmax + C1 - 1) / C1);
+  const uint32_t C2 = 8192u * (uint32_t)std::max<size_t>(1, (Mmax + 8192ull * 8192 - 1) / (8192ull * 8192));
+  const uint32_t T2max = (uint32_t)((Mmax + C2 - 1) / C2) + NH;
+  const size_t len1 = (size_t)NH * nc1, len2 = (size_t)T2max * 256;
+  uint32_t *cnt1, *okey, *oval, *binstart, *tstart, *cnt2, *bsums, *tot;
   ZK_TRY(ws.get("msm_digits", Mmax * 4, (void**)&digits));
-  ZK_TRY(ws.get("msm_counts", (size_t)K * nchunk * 4, (void**)&counts));
   ZK_TRY(ws.get("msm_bstart", (size_t)(K + 1) * 4, (void**)&bstart));
-  ZK_TRY(ws.get("msm_bsums", (size_t)nb * 4 + 16, (void**)&bsums));
   ZK_TRY(ws.get("msm_sval", Mmax * 4, (void**)&sval));
+  ZK_TRY(ws.get("msm_okey", Mmax * 4, (void**)&okey));
+  ZK_TRY(ws.get("msm_oval", Mmax * 4, (void**)&oval));
+  ZK_TRY(ws.get("msm_cnt1", len1 * 4, (void**)&cnt1));
+  ZK_TRY(ws.get("msm_cnt2", len2 * 4, (void**)&cnt2));
+  ZK_TRY(ws.get("msm_binstart", (size_t)(NH + 1) * 4, (void**)&binstart));
+  ZK_TRY(ws.get("msm_tstart", (size_t)(NH + 1) * 4, (void**)&tstart));
+  ZK_TRY(ws.get("msm_bsums", ((std::max(len1, len2) + 1023) / 1024) * 4 + 16, (void**)&bsums));
+  ZK_TRY(ws.get("msm_tot", 64, (void**)&tot));
   ZK_TRY(ws.get("msm_buckets", (size_t)K * XW * 4, (void**)&buckets));
   ZK_TRY(ws.get("msm_flags", 64 * 4, (void**)&flags));
 
@@ -1057,15 +1235,21 @@ static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, cons
     ZK_TRY(dispatch_digits(c, st, d_scalars, d_bases, G::PW, n, p, W, digits));
     ZK_HIP(hipEventRecord(lane->consumed, st));
     ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
-    dim3 grid(nchunk, W);
-    size_t lds = (B / 2) * 4;
-    k_sort_count<<<grid, SORT_THREADS, lds, st>>>(digits, ne, B, nchunk, counts);
-    k_sort_chunk_prefix<<<(K + 255) / 256, 256, 0, st>>>(counts, nchunk, B, K, bstart);
-    // exclusive scan of per-bucket totals (in bstart) -> bucket starts; bstart[K] = M
-    k_scan_blocks<<<nb, 256, 0, st>>>(bstart, K, bstart, bsums);
-    k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, bstart + K);
-    k_scan_add<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, bsums, nullptr);
-    k_sort_scatter<<<grid, SORT_THREADS, lds, st>>>(digits, ne, B, nchunk, counts, bstart, sval);
+    auto scan = [&](uint32_t* a, size_t len, uint32_t* total) {
+      uint32_t nb = (uint32_t)((len + 1023) / 1024);
+      k_scan_blocks<<<nb, 256, 0, st>>>(a, (uint32_t)len, a, bsums);
+      k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, total);
+      k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
+    };
+    k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, (uint32_t)ne, B, NH, C1, nc1, cnt1);
+    scan(cnt1, len1, &tot[0]);
+    k_rs_p1_scatter<<<nc1, RS_THREADS, rs_scatter_lds(NH), st>>>(digits, Mmax, (uint32_t)ne, B, NH, C1, nc1, cnt1, okey, oval);
+    k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, nc1, NH, &tot[0], C2, binstart, tstart);
+    ZK_HIP(hipMemsetAsync(cnt2, 0, len2 * 4, st));
+    k_rs_p2_count<<<T2max, RS_THREADS, 0, st>>>(okey, binstart, tstart, NH, C2, cnt2);
+    scan(cnt2, len2, &tot[1]);
+    k_rs_bstart<<<(K + 256) / 256, 256, 0, st>>>(cnt2, binstart, tstart, NH, K, bstart);
+    k_rs_p2_scatter<<<T2max, RS_THREADS, rs_scatter_lds(256), st>>>(okey, oval, binstart, tstart, NH, C2, cnt2, sval);
     ZK_HIP(hipGetLastError());
   }
   // level 0: fixed-size chunks of the sorted list (sized from the upper bound
