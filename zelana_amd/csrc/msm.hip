@@ -1267,7 +1267,6 @@ static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, cons
   {
     ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
     k_msm_acc0<G><<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, tn, tskip, buckets, xkey, xvalid, xpts);
-    k_msm_cutsum<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, L, buckets, xvalid, xpts, &flags[0]);
     ZK_HIP(hipGetLastError());
   }
   // segmented reduction of cut runs: level 1 pairs (tail, head) halves,
@@ -1275,6 +1274,7 @@ static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, cons
   // the previous one left nothing open (no host round-trips)
   {
     ScopedKernelTimer tm(ctx, "msm_accN", st);
+    k_msm_cutsum<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, L, buckets, xvalid, xpts, &flags[0]);
     uint32_t cur_len = (uint32_t)xl;
     for (int level = 1; cur_len > 1; level++) {
       if (level >= 63) {
