@@ -1,0 +1,186 @@
+// Host build of the device field/curve code (ff.h / ec.h are host+device):
+// the lazy G1 mixed addition xyzz_madd_g1 must give the same group element
+// as the reference-form xyzz_madd over long accumulation chains, including
+// P == Q, P == -Q, lazy X inputs and negated bases.  Prints "ok <n>".
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "../../zelana_amd/csrc/ec.h"
+
+using namespace zk;
+using F = FqOps;
+
+static uint64_t rng = 0x9E3779B97F4A7C15ull;
+static uint64_t next() {
+  rng ^= rng << 13;
+  rng ^= rng >> 7;
+  rng ^= rng << 17;
+  return rng;
+}
+static Fe inv(const Fe& a) {
+  const uint64_t e[4] = {0x3c208c16d87cfd45ull, 0x97816a916871ca8dull, 0xb85045b68181585dull, 0x30644e72e131a029ull};
+  return pow<FqP>(a, e);
+}
+static Aff<F> to_aff(const Xyzz<F>& p) {
+  Fe t = inv(mul<FqP>(p.zz, p.zzz));
+  Aff<F> a;
+  a.x = reduce<FqP>(reduce8<FqP>(mul<FqP>(p.x, mul<FqP>(t, p.zzz))));
+  a.y = reduce<FqP>(mul<FqP>(p.y, mul<FqP>(t, p.zz)));
+  return a;
+}
+static bool same(const Xyzz<F>& a, const Xyzz<F>& b) {
+  bool ia = xyzz_is_inf(a), ib = xyzz_is_inf(b);
+  if (ia || ib) return ia == ib;
+  Aff<F> x = to_aff(a), y = to_aff(b);
+  for (int i = 0; i < NL; i++)
+    if (x.x.v[i] != y.x.v[i] || x.y.v[i] != y.y.v[i]) return false;
+  return true;
+}
+
+// G2 (Fq2) chains: xyzz_madd_g2 vs the generic formula over Fq2Ops
+static const uint32_t G2GEN[32] = {
+    0xd992f6edu, 0x46debd5cu, 0xf75edaddu, 0x674322d4u, 0x5e5c4479u, 0x426a0066u, 0x121f1e76u, 0x1800deefu,
+    0xaef312c2u, 0x97e485b7u, 0x35a9e712u, 0xf1aa4933u, 0x31fb5d25u, 0x7260bfb7u, 0x920d483au, 0x198e9393u,
+    0x66fa7daau, 0x4ce6cc01u, 0x0c43d37bu, 0xe3d1e769u, 0x8dcb408fu, 0x4aab7180u, 0xdb8c6debu, 0x12c85ea5u,
+    0xd122975bu, 0x55acdadcu, 0x70b38ef3u, 0xbc4b3133u, 0x690c3395u, 0xec9e99adu, 0x585ff075u, 0x090689d0u};
+using F2 = Fq2Ops;
+static Fe2 inv2(const Fe2& a) {
+  Fe nrm = add<FqP>(sqr<FqP>(a.c0), sqr<FqP>(a.c1));
+  Fe ni = inv(nrm);
+  return Fe2{mul<FqP>(a.c0, ni), neg<FqP>(mul<FqP>(a.c1, ni))};
+}
+static Aff<F2> to_aff2(const Xyzz<F2>& p) {
+  Fe2 t = inv2(f2_mul(p.zz, p.zzz));
+  Fe2 x = f2_mul(p.x, f2_mul(t, p.zzz)), y = f2_mul(p.y, f2_mul(t, p.zz));
+  Aff<F2> a;
+  a.x = {reduce<FqP>(x.c0), reduce<FqP>(x.c1)};
+  a.y = {reduce<FqP>(y.c0), reduce<FqP>(y.c1)};
+  return a;
+}
+static bool same2(const Xyzz<F2>& a, const Xyzz<F2>& b) {
+  bool ia = xyzz_is_inf(a), ib = xyzz_is_inf(b);
+  if (ia || ib) return ia == ib;
+  Aff<F2> x = to_aff2(a), y = to_aff2(b);
+  for (int i = 0; i < NL; i++)
+    if (x.x.c0.v[i] != y.x.c0.v[i] || x.x.c1.v[i] != y.x.c1.v[i] || x.y.c0.v[i] != y.y.c0.v[i] ||
+        x.y.c1.v[i] != y.y.c1.v[i])
+      return false;
+  return true;
+}
+static int check_g2() {
+  Aff<F2> g;
+  g.x = {to_mont<FqP>(unpack(G2GEN)), to_mont<FqP>(unpack(G2GEN + 8))};
+  g.y = {to_mont<FqP>(unpack(G2GEN + 16)), to_mont<FqP>(unpack(G2GEN + 24))};
+  const int NP = 12;
+  Aff<F2> pts[NP];
+  for (int i = 0; i < NP; i++) {
+    Xyzz<F2> acc = xyzz_inf<F2>();
+    uint64_t k = next() | 1;
+    for (int b = 63; b >= 0; b--) {
+      acc = xyzz_dbl(acc);
+      if ((k >> b) & 1) acc = xyzz_madd(acc, g);
+    }
+    pts[i] = to_aff2(acc);
+  }
+  int checks = 0;
+  for (int trial = 0; trial < 60; trial++) {
+    Xyzz<F2> a = xyzz_inf<F2>(), b = xyzz_inf<F2>();
+    int len = 1 + (int)(next() % 24), prev = -1;
+    for (int s = 0; s < len; s++) {
+      int j = (int)(next() % NP);
+      bool neg_ = next() & 1;
+      uint64_t mode = next() % 6;
+      if (mode == 0 && prev >= 0) j = prev;
+      Aff<F2> qa = pts[j], qb = pts[j];
+      if (neg_) qa.y = f2_neg(qa.y);
+      qb.y = {fq_cneg(qb.y.c0, neg_), fq_cneg(qb.y.c1, neg_)};
+      a = xyzz_madd(a, qa);
+      b = xyzz_madd_g2(b, qb);
+      if (mode == 1) {
+        Aff<F2> na = qa, nb = pts[j];
+        na.y = f2_neg(qa.y);
+        nb.y = {fq_cneg(nb.y.c0, !neg_), fq_cneg(nb.y.c1, !neg_)};
+        a = xyzz_madd(a, na);
+        b = xyzz_madd_g2(b, nb);
+      }
+      prev = j;
+      if (!same2(a, b)) {
+        printf("G2 mismatch trial %d step %d\n", trial, s);
+        return -1;
+      }
+      checks++;
+    }
+    Aff<F2> q = pts[trial % NP];
+    if (!same2(xyzz_madd_g2(xyzz_from_aff(q), q), xyzz_mdbl(q))) {
+      printf("G2 doubling mismatch\n");
+      return -1;
+    }
+  }
+  return checks;
+}
+
+int main() {
+  Aff<F> g;
+  g.x = to_mont<FqP>(Fe{{1, 0, 0, 0, 0, 0, 0, 0, 0}});
+  g.y = to_mont<FqP>(Fe{{2, 0, 0, 0, 0, 0, 0, 0, 0}});
+  // table of random affine points k*G
+  const int NP = 24;
+  Aff<F> pts[NP];
+  for (int i = 0; i < NP; i++) {
+    Xyzz<F> acc = xyzz_inf<F>();
+    uint64_t k = next() | 1;
+    for (int b = 63; b >= 0; b--) {
+      acc = xyzz_dbl(acc);
+      if ((k >> b) & 1) acc = xyzz_madd(acc, g);
+    }
+    pts[i] = to_aff(acc);
+  }
+  int checks = 0;
+  for (int trial = 0; trial < 200; trial++) {
+    Xyzz<F> a = xyzz_inf<F>(), b = xyzz_inf<F>();
+    int len = 1 + (int)(next() % 40);
+    int prev = -1;
+    for (int s = 0; s < len; s++) {
+      int j = (int)(next() % NP);
+      bool neg_ = next() & 1;
+      uint64_t mode = next() % 8;
+      if (mode == 0 && prev >= 0) j = prev;  // repeated base
+      Aff<F> q = pts[j];
+      Aff<F> qa = q;
+      if (neg_) qa.y = neg<FqP>(q.y);
+      Aff<F> qb = q;
+      qb.y = fq_cneg(q.y, neg_);
+      a = xyzz_madd(a, qa);
+      b = xyzz_madd_g1(b, qb);
+      if (mode == 1) {  // cancel: add -Q right after Q
+        Aff<F> na = qa, nb = q;
+        na.y = neg<FqP>(qa.y);
+        nb.y = fq_cneg(q.y, !neg_);
+        a = xyzz_madd(a, na);
+        b = xyzz_madd_g1(b, nb);
+      }
+      prev = j;
+      if (!same(a, b)) {
+        printf("mismatch trial %d step %d\n", trial, s);
+        return 1;
+      }
+      checks++;
+    }
+    // a run that is exactly Q + Q (doubling) and Q + (-Q) (infinity)
+    Xyzz<F> d = xyzz_madd_g1(xyzz_from_aff(pts[trial % NP]), pts[trial % NP]);
+    if (!same(d, xyzz_mdbl(pts[trial % NP]))) {
+      printf("doubling mismatch\n");
+      return 1;
+    }
+    Aff<F> n = pts[trial % NP];
+    n.y = fq_cneg(n.y, true);
+    if (!xyzz_is_inf(xyzz_madd_g1(xyzz_from_aff(pts[trial % NP]), n))) {
+      printf("cancel mismatch\n");
+      return 1;
+    }
+  }
+  int c2 = check_g2();
+  if (c2 < 0) return 1;
+  printf("ok %d %d\n", checks, c2);
+  return 0;
+}

@@ -18,7 +18,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KMAP = {"msm_acc0_g1": "k_msm_acc0<zk::G1T>", "msm_acc0_g2": "k_msm_acc0<zk::G2T>"}
+KMAP = {"msm_acc0_g1": "k_msm_acc0_g1", "msm_acc0_g2": "k_msm_acc0_g2"}
 
 
 def per_launch(d, counter, sym):

@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-KMAP = {"msm_acc0_g1": "k_msm_acc0<zk::G1T>", "msm_acc0_g2": "k_msm_acc0<zk::G2T>"}
+KMAP = {"msm_acc0_g1": "k_msm_acc0_g1", "msm_acc0_g2": "k_msm_acc0_g2"}
 
 
 def main():

@@ -9,7 +9,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzkmi.so")
+LIB_PATH = os.environ.get("ZKMI_LIB") or os.path.join(HERE, "libzkmi.so")  # override: A/B builds
 
 
 class ZkmiError(RuntimeError):

@@ -14,12 +14,12 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-BUILD = os.path.join(HERE, "build")
-LIB = os.path.join(HERE, "libzkmi.so")
+BUILD = os.environ.get("ZKMI_BUILD_DIR") or os.path.join(HERE, "build")
+LIB = os.environ.get("ZKMI_LIB_OUT") or os.path.join(HERE, "libzkmi.so")
 ARCH = os.environ.get("ZKMI_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-             "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+             "-Wno-unused-variable", "-Wno-unused-but-set-variable"] + os.environ.get("ZKMI_HIPFLAGS", "").split()
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
 
 

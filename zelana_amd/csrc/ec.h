@@ -111,6 +111,75 @@ ZK_HD Xyzz<F> xyzz_madd(const Xyzz<F>& p, const Aff<F>& q) {
   return r;
 }
 
+// G1 bucket-accumulation form of madd-2008-s with lazy reduction: the same
+// group law as xyzz_madd, ~15% fewer VALU instructions.
+//   * subtractions are single-pass biased forms (subk), R is a lazy sum,
+//   * Y3 = R (Q - X3) - Y1 PPP is one two-product Montgomery pass (mul2),
+//   * X is kept in [0, 8p) across the loop (reduce8 before it is stored).
+// Every multiplication input stays inside the bounds stated in ff.h.
+// In: p.x < 8p, p.y/p.zz/p.zzz < 2p, q < 2p.  Out: x < 8p, y/zz/zzz < 2p.
+ZK_HD Xyzz<FqOps> xyzz_madd_g1(const Xyzz<FqOps>& p, const Aff<FqOps>& q) {
+  if (xyzz_is_inf(p)) return xyzz_from_aff(q);
+  Fe u2 = mul<FqP>(q.x, p.zz);
+  Fe s2 = mul<FqP>(q.y, p.zzz);
+  Fe pp_ = subk<FqP, 8>(u2, p.x);         // U2 - X1 + 8p   in (0, 10p)
+  Fe ny1 = subk<FqP, 2>(fe_zero(), p.y);  // 2p - Y1        in (0, 2p]
+  Fe rr = add_lazy(s2, ny1);              // S2 - Y1 + 2p   < 4p, limbs < 2^30
+  Fe pp = sqr<FqP>(pp_);                  // < 2p
+  if (is_zero<FqP>(pp)) {                 // U2 == X1
+    Fe rn = reduce8<FqP>(subk<FqP, 2>(s2, p.y));
+    if (is_zero<FqP>(rn)) return xyzz_mdbl(q);
+    return xyzz_inf<FqOps>();
+  }
+  Fe ppp = mul<FqP>(pp_, pp);
+  Fe qq = mul<FqP>(p.x, pp);
+  Fe t = add_lazy(add_lazy(ppp, qq), qq);  // PPP + 2Q < 6p, limbs < 3*2^29
+  Xyzz<FqOps> r;
+  r.x = subk<FqP, 6>(sqr<FqP>(rr), t);     // R^2 - PPP - 2Q + 6p in (0, 8p)
+  Fe qx = subk<FqP, 8>(qq, r.x);           // Q - X3 + 8p in (0, 10p)
+  r.y = mul2<FqP>(rr, qx, ny1, ppp);       // R (Q - X3) - Y1 PPP
+  r.zz = mul<FqP>(p.zz, pp);
+  r.zzz = mul<FqP>(p.zzz, ppp);
+  return r;
+}
+// G2 (Fq2) counterpart: lazy single-pass subtractions, Fq2 products with one
+// reduction per component, Y3 as two four-product passes.  X stays < 2p here
+// (Fq2 squares of lazy sums would leave the 169 p^2 product bound).
+// In/out: all coordinates < 2p, normalised.
+ZK_HD Xyzz<Fq2Ops> xyzz_madd_g2(const Xyzz<Fq2Ops>& p, const Aff<Fq2Ops>& q) {
+  if (xyzz_is_inf(p)) return xyzz_from_aff(q);
+  Fe2 u2 = f2_mul_n(q.x, p.zz), s2 = f2_mul_n(q.y, p.zzz);
+  Fe2 pp_ = {subk<FqP, 2>(u2.c0, p.x.c0), subk<FqP, 2>(u2.c1, p.x.c1)};  // (0, 4p)
+  Fe2 rr = {subk<FqP, 2>(s2.c0, p.y.c0), subk<FqP, 2>(s2.c1, p.y.c1)};   // (0, 4p)
+  Fe2 pp = f2_sqr_n(pp_);
+  if (f2_is_zero(pp)) {
+    if (is_zero<FqP>(reduce8<FqP>(rr.c0)) && is_zero<FqP>(reduce8<FqP>(rr.c1))) return xyzz_mdbl(q);
+    return xyzz_inf<Fq2Ops>();
+  }
+  Fe2 r2 = f2_sqr_n(rr);
+  Fe2 ppp = f2_mul_n(pp_, pp), qq = f2_mul_n(p.x, pp);
+  Xyzz<Fq2Ops> r;
+  r.x.c0 = reduce8<FqP>(subk<FqP, 6>(r2.c0, add_lazy(add_lazy(ppp.c0, qq.c0), qq.c0)));
+  r.x.c1 = reduce8<FqP>(subk<FqP, 6>(r2.c1, add_lazy(add_lazy(ppp.c1, qq.c1), qq.c1)));
+  Fe2 qx = {subk<FqP, 2>(qq.c0, r.x.c0), subk<FqP, 2>(qq.c1, r.x.c1)};  // (0, 4p)
+  Fe ny0 = subk<FqP, 2>(fe_zero(), p.y.c0), ny1 = subk<FqP, 2>(fe_zero(), p.y.c1);
+  Fe nqx1 = subk<FqP, 4>(fe_zero(), qx.c1), nppp1 = subk<FqP, 2>(fe_zero(), ppp.c1);
+  r.y.c0 = mul4<FqP>(rr.c0, qx.c0, rr.c1, nqx1, ny0, ppp.c0, ny1, nppp1);
+  r.y.c1 = mul4<FqP>(rr.c0, qx.c1, rr.c1, qx.c0, ny0, ppp.c1, ny1, ppp.c0);
+  r.zz = f2_mul_n(p.zz, pp);
+  r.zzz = f2_mul_n(p.zzz, ppp);
+  return r;
+}
+
+// conditional negation of an affine y (< 2p) without a borrow/fix-up pass
+ZK_HD Fe fq_cneg(const Fe& y, bool neg_) {
+  Fe n = subk<FqP, 2>(fe_zero(), y);
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = neg_ ? n.v[i] : y.v[i];
+  return r;
+}
+
 // P + Q   (add-2008-s)
 template <class F>
 ZK_HD Xyzz<F> xyzz_add(const Xyzz<F>& p, const Xyzz<F>& q) {

@@ -43,6 +43,13 @@ struct FqP {
                                        0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};  // R mod p
   static constexpr uint32_t R2[NL] = {0x059bac10u, 0x0d1503a3u, 0x018016b8u, 0x10ab0ca8u, 0x02632639u,
                                       0x02c0169fu, 0x169bfd53u, 0x11869d4cu, 0x002a11a6u};  // R^2 mod p
+  // 4p, 6p, 8p in normalised limbs (biases of the lazy subtractions)
+  static constexpr uint32_t P4[NL] = {0x01f3f51cu, 0x041182dbu, 0x11ca8d3cu, 0x0b548b43u, 0x161765e0u,
+                                      0x0b6d0302u, 0x029b8504u, 0x197098d0u, 0x00c19139u};
+  static constexpr uint32_t P6[NL] = {0x12edefaau, 0x061a4448u, 0x0aafd3dau, 0x10fed0e5u, 0x012318d0u,
+                                      0x11238484u, 0x03e94786u, 0x1628e538u, 0x012259d6u};
+  static constexpr uint32_t P8[NL] = {0x03e7ea38u, 0x082305b6u, 0x03951a78u, 0x16a91687u, 0x0c2ecbc0u,
+                                      0x16da0605u, 0x05370a08u, 0x12e131a0u, 0x01832273u};
 };
 // Scalar field r (NTT domain)
 struct FrP {
@@ -97,6 +104,26 @@ ZK_HD Fe fe_zero() {
   return r;
 }
 
+// ------------------------------------------------------- column accumulate
+// acc += a * b as exactly one v_mad_u64_u32 on the device.  Written as inline
+// asm so that every column stays ONE dependent chain: left to itself the
+// compiler splits columns into parallel partial sums (to hide mad latency a
+// single wave would see) and pays a 64-bit add per split, ~9% of a
+// multiplication; with 3-4 waves per SIMD the latency is already hidden.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(ZK_NO_ASM_MAD)
+__device__ __forceinline__ void mac(uint64_t& acc, uint32_t a, uint32_t b) {
+  uint64_t cy;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cy) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void macs(uint64_t& acc, uint32_t a, uint32_t b_uniform) {
+  uint64_t cy;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cy) : "v"(a), "s"(b_uniform));
+}
+#else
+ZK_HD void mac(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b; }
+ZK_HD void macs(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b; }
+#endif
+
 // ------------------------------------------------------------ Montgomery mul
 // r = a*b*2^-261 mod p (lazy: result < 2p, normalised limbs).
 template <class P>
@@ -108,20 +135,20 @@ ZK_HD Fe mul(const Fe& a, const Fe& b) {
   for (int k = 0; k < NL; k++) {
 #pragma unroll
     for (int j = 0; j < k; j++) {
-      acc += (uint64_t)a.v[j] * b.v[k - j];
-      acc += (uint64_t)m[j] * P::P[k - j];
+      mac(acc, a.v[j], b.v[k - j]);
+      macs(acc, m[j], P::P[k - j]);
     }
-    acc += (uint64_t)a.v[k] * b.v[0];
+    mac(acc, a.v[k], b.v[0]);
     m[k] = ((uint32_t)acc * P::PINV) & LMASK;
-    acc += (uint64_t)m[k] * P::P[0];
+    macs(acc, m[k], P::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
 #pragma unroll
     for (int j = k - (NL - 1); j < NL; j++) {
-      acc += (uint64_t)a.v[j] * b.v[k - j];
-      acc += (uint64_t)m[j] * P::P[k - j];
+      mac(acc, a.v[j], b.v[k - j]);
+      macs(acc, m[j], P::P[k - j]);
     }
     r.v[k - NL] = (uint32_t)acc & LMASK;
     acc >>= 29;
@@ -141,21 +168,21 @@ ZK_HD Fe sqr(const Fe& a) {
 #pragma unroll
   for (int k = 0; k < NL; k++) {
 #pragma unroll
-    for (int j = 0; j < (k + 1) / 2; j++) acc += (uint64_t)d[j] * a.v[k - j];
-    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+    for (int j = 0; j < (k + 1) / 2; j++) mac(acc, d[j], a.v[k - j]);
+    if ((k & 1) == 0) mac(acc, a.v[k / 2], a.v[k / 2]);
 #pragma unroll
-    for (int j = 0; j < k; j++) acc += (uint64_t)m[j] * P::P[k - j];
+    for (int j = 0; j < k; j++) macs(acc, m[j], P::P[k - j]);
     m[k] = ((uint32_t)acc * P::PINV) & LMASK;
-    acc += (uint64_t)m[k] * P::P[0];
+    macs(acc, m[k], P::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
 #pragma unroll
-    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) acc += (uint64_t)d[j] * a.v[k - j];
-    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) mac(acc, d[j], a.v[k - j]);
+    if ((k & 1) == 0) mac(acc, a.v[k / 2], a.v[k / 2]);
 #pragma unroll
-    for (int j = k - (NL - 1); j < NL; j++) acc += (uint64_t)m[j] * P::P[k - j];
+    for (int j = k - (NL - 1); j < NL; j++) macs(acc, m[j], P::P[k - j]);
     r.v[k - NL] = (uint32_t)acc & LMASK;
     acc >>= 29;
   }
@@ -221,6 +248,227 @@ ZK_HD Fe add_lazy(const Fe& a, const Fe& b) {
 #pragma unroll
   for (int i = 0; i < NL; i++) r.v[i] = a.v[i] + b.v[i];
   return r;
+}
+
+// ---------------------------------------------------------- lazy forms
+// Bounds used by the fast G1 mixed addition (R/p = 169.3, so a Montgomery
+// product of values a, b with a*b < 169 p^2 still lands in [0, 2p); columns
+// stay below 2^64 while one factor's limbs are < 2^30 and the other's < 2^29,
+// or both < 2^30 for a single product).
+//
+// a - b + K p in one signed-carry pass: normalised limbs, value a - b + Kp.
+// Caller guarantees 0 <= a - b + Kp < 2^261 (limbs of a, b may be up to 2^31).
+template <class P, int K>
+ZK_HD Fe subk(const Fe& a, const Fe& b) {
+  static_assert(K == 2 || K == 4 || K == 6 || K == 8, "bias");
+  const uint32_t* kp = K == 2 ? P::P2 : K == 4 ? P::P4 : K == 6 ? P::P6 : P::P8;
+  Fe r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    int32_t t = (int32_t)(a.v[i] + kp[i]) - (int32_t)b.v[i] + c;
+    r.v[i] = (uint32_t)t & LMASK;
+    c = t >> 29;
+  }
+  return r;
+}
+// (a*b + c*d) * 2^-261 mod p in one product-scanning pass (one reduction for
+// two products).  a, c: limbs < 2^30; b, d: limbs < 2^29; a*b + c*d < 169 p^2.
+template <class P>
+ZK_HD Fe mul2(const Fe& a, const Fe& b, const Fe& c, const Fe& d) {
+  uint32_t m[NL];
+  Fe r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      mac(acc, a.v[j], b.v[k - j]);
+      mac(acc, c.v[j], d.v[k - j]);
+      macs(acc, m[j], P::P[k - j]);
+    }
+    mac(acc, a.v[k], b.v[0]);
+    mac(acc, c.v[k], d.v[0]);
+    m[k] = ((uint32_t)acc * P::PINV) & LMASK;
+    macs(acc, m[k], P::P[0]);
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) {
+      mac(acc, a.v[j], b.v[k - j]);
+      mac(acc, c.v[j], d.v[k - j]);
+      macs(acc, m[j], P::P[k - j]);
+    }
+    r.v[k - NL] = (uint32_t)acc & LMASK;
+    acc >>= 29;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+  return r;
+}
+// Two independent Montgomery products interleaved column by column: two
+// accumulator chains in one instruction stream give each wave the ILP that a
+// single dependent mad chain lacks.
+template <class P>
+ZK_HD void mul_x2(const Fe& a, const Fe& b, const Fe& c, const Fe& d, Fe& r0, Fe& r1) {
+  uint32_t m[NL], n[NL];
+  uint64_t x = 0, y = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      mac(x, a.v[j], b.v[k - j]);
+      mac(y, c.v[j], d.v[k - j]);
+      macs(x, m[j], P::P[k - j]);
+      macs(y, n[j], P::P[k - j]);
+    }
+    mac(x, a.v[k], b.v[0]);
+    mac(y, c.v[k], d.v[0]);
+    m[k] = ((uint32_t)x * P::PINV) & LMASK;
+    n[k] = ((uint32_t)y * P::PINV) & LMASK;
+    macs(x, m[k], P::P[0]);
+    macs(y, n[k], P::P[0]);
+    x >>= 29;
+    y >>= 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) {
+      mac(x, a.v[j], b.v[k - j]);
+      mac(y, c.v[j], d.v[k - j]);
+      macs(x, m[j], P::P[k - j]);
+      macs(y, n[j], P::P[k - j]);
+    }
+    r0.v[k - NL] = (uint32_t)x & LMASK;
+    r1.v[k - NL] = (uint32_t)y & LMASK;
+    x >>= 29;
+    y >>= 29;
+  }
+  r0.v[NL - 1] = (uint32_t)x;
+  r1.v[NL - 1] = (uint32_t)y;
+}
+template <class P>
+ZK_HD void sqr_x2(const Fe& a, const Fe& c, Fe& r0, Fe& r1) {
+  uint32_t m[NL], n[NL], da[NL], dc[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    da[i] = a.v[i] << 1;
+    dc[i] = c.v[i] << 1;
+  }
+  uint64_t x = 0, y = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int j = 0; j < (k + 1) / 2; j++) {
+      mac(x, da[j], a.v[k - j]);
+      mac(y, dc[j], c.v[k - j]);
+    }
+    if ((k & 1) == 0) {
+      mac(x, a.v[k / 2], a.v[k / 2]);
+      mac(y, c.v[k / 2], c.v[k / 2]);
+    }
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      macs(x, m[j], P::P[k - j]);
+      macs(y, n[j], P::P[k - j]);
+    }
+    m[k] = ((uint32_t)x * P::PINV) & LMASK;
+    n[k] = ((uint32_t)y * P::PINV) & LMASK;
+    macs(x, m[k], P::P[0]);
+    macs(y, n[k], P::P[0]);
+    x >>= 29;
+    y >>= 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) {
+      mac(x, da[j], a.v[k - j]);
+      mac(y, dc[j], c.v[k - j]);
+    }
+    if ((k & 1) == 0) {
+      mac(x, a.v[k / 2], a.v[k / 2]);
+      mac(y, c.v[k / 2], c.v[k / 2]);
+    }
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) {
+      macs(x, m[j], P::P[k - j]);
+      macs(y, n[j], P::P[k - j]);
+    }
+    r0.v[k - NL] = (uint32_t)x & LMASK;
+    r1.v[k - NL] = (uint32_t)y & LMASK;
+    x >>= 29;
+    y >>= 29;
+  }
+  r0.v[NL - 1] = (uint32_t)x;
+  r1.v[NL - 1] = (uint32_t)y;
+}
+
+// (a*b + c*d + e*f + g*h) * 2^-261 mod p: four products, one reduction.
+// All operand limbs < 2^29 (normalised); sum of products < 169 p^2.
+template <class P>
+ZK_HD Fe mul4(const Fe& a, const Fe& b, const Fe& c, const Fe& d, const Fe& e, const Fe& f, const Fe& g,
+              const Fe& h) {
+  uint32_t m[NL];
+  Fe r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      mac(acc, a.v[j], b.v[k - j]);
+      mac(acc, c.v[j], d.v[k - j]);
+      mac(acc, e.v[j], f.v[k - j]);
+      mac(acc, g.v[j], h.v[k - j]);
+      macs(acc, m[j], P::P[k - j]);
+    }
+    mac(acc, a.v[k], b.v[0]);
+    mac(acc, c.v[k], d.v[0]);
+    mac(acc, e.v[k], f.v[0]);
+    mac(acc, g.v[k], h.v[0]);
+    m[k] = ((uint32_t)acc * P::PINV) & LMASK;
+    macs(acc, m[k], P::P[0]);
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) {
+      mac(acc, a.v[j], b.v[k - j]);
+      mac(acc, c.v[j], d.v[k - j]);
+      mac(acc, e.v[j], f.v[k - j]);
+      mac(acc, g.v[j], h.v[k - j]);
+      macs(acc, m[j], P::P[k - j]);
+    }
+    r.v[k - NL] = (uint32_t)acc & LMASK;
+    acc >>= 29;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+// [0, 8p) -> [0, 2p), normalised limbs
+template <class P>
+ZK_HD Fe reduce8(const Fe& a) {
+  Fe x = a;
+#pragma unroll
+  for (int step = 0; step < 2; step++) {
+    const uint32_t* kp = step == 0 ? P::P4 : P::P2;
+    Fe d;
+    int32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < NL; i++) {
+      int32_t t = (int32_t)x.v[i] - (int32_t)kp[i] + br;
+      d.v[i] = (uint32_t)t & LMASK;
+      br = t >> 29;
+    }
+    const bool neg_ = br < 0;
+#pragma unroll
+    for (int i = 0; i < NL; i++) x.v[i] = neg_ ? x.v[i] : d.v[i];
+  }
+  return x;
 }
 
 // fully reduce [0, 2p) -> [0, p)
@@ -315,6 +563,16 @@ ZK_HD bool fe_is_zero_raw(const Fe& a) {
 }
 ZK_HD Fe2 f2_zero() { return {fe_zero(), fe_zero()}; }
 ZK_HD Fe2 f2_one() { return {one<FqP>(), fe_zero()}; }
+
+// Fq2 products with one reduction per component (mul2): inputs normalised
+// limbs, values < 4p; outputs < 2p.
+ZK_HD Fe2 f2_mul_n(const Fe2& a, const Fe2& b) {
+  Fe nb1 = subk<FqP, 4>(fe_zero(), b.c1);
+  return {mul2<FqP>(a.c0, b.c0, a.c1, nb1), mul2<FqP>(a.c0, b.c1, a.c1, b.c0)};
+}
+ZK_HD Fe2 f2_sqr_n(const Fe2& a) {
+  return {mul<FqP>(add_lazy(a.c0, a.c1), subk<FqP, 4>(a.c0, a.c1)), mul<FqP>(add_lazy(a.c0, a.c0), a.c1)};
+}
 
 // Uniform field interface used by the curve templates.
 struct FqOps {

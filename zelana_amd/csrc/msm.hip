@@ -25,6 +25,7 @@
 //                     over a (high, low) split of the bucket index.
 //   7. host Horner    sum_k 2^k V_k over the ~256 bit sums (msm_host.cpp).
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -494,8 +495,15 @@ __global__ void __launch_bounds__(256) k_msm_cutsum(const uint32_t* __restrict__
   st_xyzz<G>(buckets + (size_t)b * XW, sum);
 }
 
+// accumulator store: G1 keeps X lazily in [0, 8p) inside the loop
 template <class G>
-__global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bstart,
+__device__ __forceinline__ void st_acc(uint32_t* p, Xyzz<typename G::F> v) {
+  if constexpr (G::CW == 8) v.x = reduce8<FqP>(v.x);
+  st_xyzz<G>(p, v);
+}
+
+template <class G>
+__device__ __forceinline__ void msm_acc0_body(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bstart,
                                                   uint32_t K, uint32_t L, uint32_t nchunks,
                                                   const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
                                                   uint32_t* __restrict__ buckets,
@@ -527,16 +535,53 @@ __global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ s
   bool head_done = false, tail_done = false;
   Xyzz<F> acc = xyzz_inf<F>();
   bool first_run = true;
+  // Software pipeline: the sorted entry two ahead and the base one ahead are
+  // in flight while the current mixed addition runs (one gather latency per
+  // entry would otherwise be exposed to the few waves a SIMD holds).
+  constexpr int PQ = G::PW / 4;  // 16-B words per affine base
+  auto row = [&](uint32_t v) {
+    uint32_t idx = v & 0x7FFFFFFFu;
+    if (tskip) idx += (idx / tn) * tskip;  // entry j*n + i -> table row j*N + i
+    return reinterpret_cast<const uint4*>(bases + (size_t)idx * G::PW);
+  };
+  // (G2 prefetches only the entry: a second 128-B base in flight would cost
+  // the second wave per SIMD that 256 VGPRs allow.)
+  constexpr bool PF = G::CW == 8;
+  uint32_t v_nxt = sval[start];
+  uint4 raw[PQ];
+  if constexpr (PF) {
+    const uint4* q = row(v_nxt);
+#pragma unroll
+    for (int k = 0; k < PQ; k++) raw[k] = q[k];
+  }
+  uint32_t v_nn = start + 1 < end ? sval[start + 1] : 0u;
   for (uint32_t p = start; p < end; p++) {
+    uint4 cr[PQ];
+    const uint32_t v = v_nxt;
+    if constexpr (PF) {
+#pragma unroll
+      for (int k = 0; k < PQ; k++) cr[k] = raw[k];
+      if (p + 1 < end) {
+        const uint4* q = row(v_nn);
+#pragma unroll
+        for (int k = 0; k < PQ; k++) raw[k] = q[k];
+      }
+    } else {
+      const uint4* q = row(v);
+#pragma unroll
+      for (int k = 0; k < PQ; k++) cr[k] = q[k];
+    }
+    v_nxt = v_nn;
+    if (p + 2 < end) v_nn = sval[p + 2];
     if (p == next_b) {
       // run of `cur` ends here (complete on the right)
       if (first_run && left_cut) {
         xkey[2 * t + 1] = cur;
         xvalid[2 * t + 1] = 1;
-        st_xyzz<G>(xpts + (size_t)(2 * t + 1) * XW, acc);
+        st_acc<G>(xpts + (size_t)(2 * t + 1) * XW, acc);
         head_done = true;
       } else {
-        st_xyzz<G>(buckets + (size_t)cur * XW, acc);
+        st_acc<G>(buckets + (size_t)cur * XW, acc);
       }
       acc = xyzz_inf<F>();
       first_run = false;
@@ -545,12 +590,17 @@ __global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ s
         next_b = bstart[cur + 1];
       } while (next_b == p);  // skip empty buckets
     }
-    uint32_t v = sval[p];
-    uint32_t idx = v & 0x7FFFFFFFu;
-    if (tskip) idx += (idx / tn) * tskip;  // entry j*n + i -> table row j*N + i
-    Aff<F> P = ld_aff<G>(bases, idx);
-    if (v >> 31) P.y = F::neg(P.y);
-    acc = xyzz_madd(acc, P);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(cr);
+    Aff<F> P;
+    if constexpr (G::CW == 8) {
+      P.x = unpack(w);
+      P.y = fq_cneg(unpack(w + 8), v >> 31);
+      acc = xyzz_madd_g1(acc, P);
+    } else {
+      P.x = {unpack(w), unpack(w + 8)};
+      P.y = {fq_cneg(unpack(w + 16), v >> 31), fq_cneg(unpack(w + 24), v >> 31)};
+      acc = xyzz_madd_g2(acc, P);
+    }
   }
   const bool left_open = first_run && left_cut;
   const bool right_open = next_b > end;
@@ -558,11 +608,11 @@ __global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ s
     const uint32_t slot = left_open ? 2 * t + 1 : 2 * t + 2;
     xkey[slot] = cur;
     xvalid[slot] = 1;
-    st_xyzz<G>(xpts + (size_t)slot * XW, acc);
+    st_acc<G>(xpts + (size_t)slot * XW, acc);
     if (left_open) head_done = true;
     else tail_done = true;
   } else {
-    st_xyzz<G>(buckets + (size_t)cur * XW, acc);
+    st_acc<G>(buckets + (size_t)cur * XW, acc);
   }
   if (!head_done) {
     xkey[2 * t + 1] = first_key;
@@ -573,6 +623,37 @@ __global__ void __launch_bounds__(256) k_msm_acc0(const uint32_t* __restrict__ s
     xvalid[2 * t + 2] = 0;
   }
 }
+
+// G1 bodies fit 128 VGPRs (4 waves per SIMD) only with a minimum-occupancy
+// hint; G2 needs ~300 and keeps the default.
+#ifndef ZK_ACC0_G2_MINBLK
+#define ZK_ACC0_G2_MINBLK 2
+#endif
+#ifndef ZK_ACC0_G1_MINBLK
+#define ZK_ACC0_G1_MINBLK 1
+#endif
+__global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK) k_msm_acc0_g1(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bstart,
+                                                  uint32_t K, uint32_t L, uint32_t nchunks,
+                                                  const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
+                                                  uint32_t* __restrict__ buckets,
+                                                  uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
+                                                  uint32_t* __restrict__ xpts) { msm_acc0_body<G1T>(sval, bstart, K, L, nchunks, bases, tn, tskip, buckets, xkey, xvalid, xpts); }
+__global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK) k_msm_acc0_g2(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bstart,
+                                                  uint32_t K, uint32_t L, uint32_t nchunks,
+                                                  const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
+                                                  uint32_t* __restrict__ buckets,
+                                                  uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
+                                                  uint32_t* __restrict__ xpts) { msm_acc0_body<G2T>(sval, bstart, K, L, nchunks, bases, tn, tskip, buckets, xkey, xvalid, xpts); }
+template <class G>
+struct Acc0Kernel;
+template <>
+struct Acc0Kernel<G1T> {
+  static constexpr auto fn = k_msm_acc0_g1;
+};
+template <>
+struct Acc0Kernel<G2T> {
+  static constexpr auto fn = k_msm_acc0_g2;
+};
 
 template <class G>
 __global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ xkey, const uint32_t* __restrict__ xvalid,
@@ -1253,8 +1334,16 @@ static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, cons
     ZK_HIP(hipGetLastError());
   }
   // level 0: fixed-size chunks of the sorted list (sized from the upper bound
-  // W*n so no host round-trip is needed; chunks past M exit at once)
-  uint32_t L = (uint32_t)std::max<size_t>(4, (Mmax + (size_t)ctx->num_cus * 1024 - 1) / ((size_t)ctx->num_cus * 1024));
+  // W*n so no host round-trip is needed; chunks past M exit at once).
+  // Threads per CU: measured best at ~1024 for G1 (over-subscribing the
+  // resident waves evens out per-thread run lengths); ZKMI_ACC_TPC overrides.
+  static const size_t tpc_env = [] {
+    const char* e = getenv("ZKMI_ACC_TPC");
+    return e ? (size_t)atol(e) : (size_t)0;
+  }();
+  const size_t tpc = tpc_env ? tpc_env : 1024;
+  const size_t acc_threads = (size_t)ctx->num_cus * tpc;
+  uint32_t L = (uint32_t)std::max<size_t>(4, (Mmax + acc_threads - 1) / acc_threads);
   uint32_t nch = (uint32_t)((Mmax + L - 1) / L);
   uint32_t *xkey, *xvalid, *xpts, *ykey, *yvalid, *ypts;
   size_t xl = 2 * (size_t)nch + 1;
@@ -1266,7 +1355,7 @@ static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, cons
   ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
   {
     ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
-    k_msm_acc0<G><<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, tn, tskip, buckets, xkey, xvalid, xpts);
+    Acc0Kernel<G>::fn<<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, tn, tskip, buckets, xkey, xvalid, xpts);
     ZK_HIP(hipGetLastError());
   }
   // segmented reduction of cut runs: level 1 pairs (tail, head) halves,
