@@ -120,6 +120,12 @@ int zkmi_msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const voi
                     zkmi_msm_job** job);
 int zkmi_msm_wait(zkmi_msm_job* job, uint64_t* out_affine);
 /* window size override for experiments (0 = automatic) */
+/* k MSMs with the same device scalars and range over k base sets (e.g. a,
+ * b_g1 and b_g2 queries of a proving key, all weighted by z): one digits +
+ * sort pass is shared by every set with the same window plan.  jobs[i] is the
+ * job of bs[i] (finish each with zkmi_msm_wait). */
+int zkmi_msm_submit_shared(zkmi_ctx* ctx, const zkmi_bases* const* bs, int k, size_t offset, const void* d_scalars,
+                           size_t n, zkmi_msm_job** jobs);
 int zkmi_msm_set_window(zkmi_ctx* ctx, int c);
 /* Number of MSM lanes (streams with their own scratch) used round-robin by
  * consecutive submissions so their latency-bound tails overlap; 1..8. */

@@ -229,3 +229,28 @@ def test_msm_table_2pow16_and_pipelined(ctx):
     sc2 = np.zeros((20000, 4), np.uint64)
     d.download(sc2)
     assert np.array_equal(ctx.msm_wait(jobs[1]), O.msm_g1(g.export()[:19000], sc2[:19000]))
+
+
+def test_msm_shared_sort(ctx):
+    """One sort shared by G1/G2 base sets (different infinity positions, one
+    set with a table): every result equals its own oracle MSM."""
+    from zelana_amd.gpu import DeviceBuffer
+    n = 2500
+    p1 = O.gen_points_g1(61, n)
+    p1[5:9] = 0
+    p2 = O.gen_points_g1(62, n)
+    p2[100:140] = 0
+    q2 = O.gen_points_g2(63, n)
+    q2[7] = 0
+    sc = _rand_scalars(np.random.default_rng(64), n - 3, "witness")
+    d = DeviceBuffer(ctx, sc.nbytes)
+    d.upload(sc)
+    b1, b2, g2 = ctx.bases_g1(p1), ctx.bases_g1(p2), ctx.bases_g2(q2)
+    t3 = ctx.bases_g1(p2)
+    t3.precompute()  # different plan: sorted separately
+    jobs = ctx.msm_submit_shared([b1, b2, g2, t3], d, n - 3, offset=2)
+    got = [ctx.msm_wait(j) for j in jobs]
+    assert np.array_equal(got[0], O.msm_g1(p1[2:n - 1], sc))
+    assert np.array_equal(got[1], O.msm_g1(p2[2:n - 1], sc))
+    assert np.array_equal(got[2], O.msm_g2(q2[2:n - 1], sc))
+    assert np.array_equal(got[3], O.msm_g1(p2[2:n - 1], sc))

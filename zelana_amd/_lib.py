@@ -65,6 +65,7 @@ SIGNATURES = [
     ("zkmi_msm_wait", ctypes.c_int, [vp, u64p]),
     ("zkmi_msm_set_window", ctypes.c_int, [vp, ctypes.c_int]),
     ("zkmi_msm_set_lanes", ctypes.c_int, [vp, ctypes.c_int]),
+    ("zkmi_msm_submit_shared", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_int, sz, vp, sz, ctypes.POINTER(vp)]),
     ("zkmi_g1_add", ctypes.c_int, [u64p, u64p, u64p]),
     ("zkmi_g2_add", ctypes.c_int, [u64p, u64p, u64p]),
     ("zkmi_ntt", ctypes.c_int, [vp, u64p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),

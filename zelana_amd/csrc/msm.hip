@@ -125,24 +125,24 @@ __device__ __forceinline__ void scalar_digits(const uint32_t* __restrict__ scala
   }
 }
 
-// Signed digits of every scalar, once per MSM (int32, 0 = nothing to add;
-// bases at infinity get all-zero digits).  Window w = j*Wp + w' of the plain
-// recoding is digit w' of table copy j: digits[(w' * p + j) * n + i], so the
-// sort sees Wp windows of p*n entries (p = 1, Wp = W without a table).
+// Signed digits of every scalar, once per MSM (int32, 0 = nothing to add).
+// Window w = j*Wp + w' of the plain recoding is digit w' of table copy j:
+// digits[(w' * p + j) * n + i], so the sort sees Wp windows of p*n entries
+// (p = 1, Wp = W without a table).  Digits depend on the scalars only (bases
+// at infinity are skipped in the accumulation), so MSMs with the same
+// scalars over different base sets share one sort (msm_submit_shared).
 template <int C>
-__global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars,
-                                                    const uint32_t* __restrict__ bases, int pw, size_t n, int p,
-                                                    int Wp, int32_t* __restrict__ digits) {
+__global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars, size_t n, int p, int Wp,
+                                                    int32_t* __restrict__ digits) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   constexpr int W = msm_windows(C);
   int32_t d[W];
   scalar_digits<C>(scalars, i, d);
-  const bool inf = bases[i * pw + pw - 1] >> 31;
 #pragma unroll
   for (int w = 0; w < W; w++) {
     int j = w / Wp, wq = w - j * Wp;
-    digits[((size_t)wq * p + j) * n + i] = inf ? 0 : d[w];
+    digits[((size_t)wq * p + j) * n + i] = d[w];
   }
   for (int w = W; w < p * Wp; w++) {
     int j = w / Wp, wq = w - j * Wp;
@@ -502,6 +502,10 @@ __device__ __forceinline__ void st_acc(uint32_t* p, Xyzz<typename G::F> v) {
   st_xyzz<G>(p, v);
 }
 
+#ifdef ZK_ACC0_TRACE
+// dev-only (variant builds): per-wave start/end realtime and hardware ids
+__device__ uint64_t zk_acc0_trace[4 * 65536];
+#endif
 template <class G>
 __device__ __forceinline__ void msm_acc0_body(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bstart,
                                                   uint32_t K, uint32_t L, uint32_t nchunks,
@@ -513,6 +517,25 @@ __device__ __forceinline__ void msm_acc0_body(const uint32_t* __restrict__ sval,
   constexpr int XW = 4 * G::CW;
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nchunks) return;
+#ifdef ZK_ACC0_TRACE
+  const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
+  struct TraceEnd {
+    uint32_t t;
+    uint64_t t0;
+    __device__ ~TraceEnd() {
+      if ((t & 63) == 0 && (t >> 6) < 65536) {
+        uint32_t xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        uint64_t* r = zk_acc0_trace + 4 * (t >> 6);
+        r[0] = t0;
+        r[1] = __builtin_amdgcn_s_memrealtime();
+        r[2] = xcc;
+        r[3] = hw;
+      }
+    }
+  } trace_end{t, tr0};
+#endif
   const uint32_t M = bstart[K];
   uint32_t start = t * L;
   if (t == 0) {
@@ -591,6 +614,7 @@ __device__ __forceinline__ void msm_acc0_body(const uint32_t* __restrict__ sval,
       } while (next_b == p);  // skip empty buckets
     }
     const uint32_t* w = reinterpret_cast<const uint32_t*>(cr);
+    if (w[G::PW - 1] >> 31) continue;  // base at infinity: adds nothing
     Aff<F> P;
     if constexpr (G::CW == 8) {
       P.x = unpack(w);
@@ -1200,15 +1224,13 @@ static int pick_window(size_t n) {
 }
 
 template <int C>
-static void launch_digits(hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw, size_t n, int p, int Wp,
-                          int32_t* dg) {
-  k_msm_digits<C><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(sc, bases, pw, n, p, Wp, dg);
+static void launch_digits(hipStream_t st, const uint32_t* sc, size_t n, int p, int Wp, int32_t* dg) {
+  k_msm_digits<C><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(sc, n, p, Wp, dg);
 }
-static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, const uint32_t* bases, int pw, size_t n, int p,
-                           int Wp, int32_t* dg) {
+static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, size_t n, int p, int Wp, int32_t* dg) {
   switch (c) {
 #define ZK_C(CC) \
-  case CC: launch_digits<CC>(st, sc, bases, pw, n, p, Wp, dg); break;
+  case CC: launch_digits<CC>(st, sc, n, p, Wp, dg); break;
     ZK_C(4) ZK_C(5) ZK_C(6) ZK_C(7) ZK_C(8) ZK_C(9) ZK_C(10) ZK_C(11) ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15)
     ZK_C(16) ZK_C(17)
 #undef ZK_C
@@ -1255,45 +1277,49 @@ static int get_lane(zkmi_ctx* ctx, MsmLane** out) {
   return 0;
 }
 
-template <class G>
-static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, const uint32_t* d_scalars, size_t n,
-                        zkmi_msm_job** out_job) {
-  constexpr int XW = 4 * G::CW;
-  MsmLane* lane = nullptr;
-  ZK_TRY(get_lane(ctx, &lane));
-  hipStream_t st = lane->st;
-  Workspace& ws = lane->ws;
-  const uint32_t* d_bases = tb->d_pts + offset * G::PW;
+// Window / table plan of one MSM over base set tb.
+struct MsmPlan {
+  int c, p, W, bb, lb, hb;
+  size_t ne, Mmax;
+  uint32_t B, K;
+};
+static MsmPlan msm_plan(const zkmi_ctx* ctx, const zkmi_bases* tb, size_t n) {
+  MsmPlan P;
   // a fixed-base table is used when the caller did not pin another window
   const bool table = tb->tc > 0 && (ctx->msm_window == 0 || ctx->msm_window == tb->tc);
-  const int c = table ? tb->tc : (ctx->msm_window > 0 ? ctx->msm_window : pick_window(n));
-  const int p = table ? tb->tp : 1;
-  const int W = table ? tb->tw : msm_windows(c);  // windows actually run
-  const size_t ne = (size_t)p * n;                  // entries per window
-  uint32_t B = 1u << (c - 1);
-  uint32_t K = (uint32_t)W * B;
-  int bb = c - 1, lb = (bb + 1) / 2, hb = bb - lb;
-  zkmi_msm_job* job = new zkmi_msm_job{ctx, G::CW == 16, c, W, bb, nullptr, 0, nullptr, n == 0};
-  *out_job = job;
-  if (n == 0) return 0;
-  if (ne >= (1u << 31) || (size_t)W * ne >= (1ull << 32)) {
-    set_error("MSM size %zu too large for one call", n);
-    return ZKMI_EINVAL;
-  }
-  const uint32_t tn = (uint32_t)n, tskip = p > 1 ? (uint32_t)(tb->n - n) : 0u;
-  uint32_t *bstart, *sval, *buckets, *flags;
-  int32_t* digits;
-  size_t Mmax = (size_t)W * ne;
+  P.c = table ? tb->tc : (ctx->msm_window > 0 ? ctx->msm_window : pick_window(n));
+  P.p = table ? tb->tp : 1;
+  P.W = table ? tb->tw : msm_windows(P.c);  // windows actually run
+  P.ne = (size_t)P.p * n;                   // entries per window
+  P.Mmax = (size_t)P.W * P.ne;
+  P.B = 1u << (P.c - 1);
+  P.K = (uint32_t)P.W * P.B;
+  P.bb = P.c - 1;
+  P.lb = (P.bb + 1) / 2;
+  P.hb = P.bb - P.lb;
+  return P;
+}
+static bool same_plan(const MsmPlan& a, const MsmPlan& b) { return a.c == b.c && a.p == b.p && a.W == b.W; }
+
+// Digits + bucket sort on the lane stream: sval (sorted entries) and bstart
+// (K + 1 bucket starts) in the lane workspace.  The context stream waits only
+// for the digits pass, the one reader of the scalars.
+static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const uint32_t* d_scalars, size_t n,
+                          uint32_t** out_sval, uint32_t** out_bstart) {
+  hipStream_t st = lane->st;
+  Workspace& ws = lane->ws;
+  const uint32_t NH = (P.K + 255) >> RS_LO;
+  const size_t Mmax = P.Mmax;
   // radix-sort geometry (see k_rs_*): ~2K P1 chunks, ~8K P2 tiles at most
-  const uint32_t NH = (K + 255) >> RS_LO;
   const uint32_t C1 = 16384u * (uint32_t)std::max<size_t>(1, (Mmax + 16384ull * 2048 - 1) / (16384ull * 2048));
   const uint32_t nc1 = (uint32_t)((Mmax + C1 - 1) / C1);
   const uint32_t C2 = 8192u * (uint32_t)std::max<size_t>(1, (Mmax + 8192ull * 8192 - 1) / (8192ull * 8192));
   const uint32_t T2max = (uint32_t)((Mmax + C2 - 1) / C2) + NH;
   const size_t len1 = (size_t)NH * nc1, len2 = (size_t)T2max * 256;
-  uint32_t *cnt1, *okey, *oval, *binstart, *tstart, *cnt2, *bsums, *tot;
+  int32_t* digits;
+  uint32_t *bstart, *sval, *cnt1, *okey, *oval, *binstart, *tstart, *cnt2, *bsums, *tot;
   ZK_TRY(ws.get("msm_digits", Mmax * 4, (void**)&digits));
-  ZK_TRY(ws.get("msm_bstart", (size_t)(K + 1) * 4, (void**)&bstart));
+  ZK_TRY(ws.get("msm_bstart", (size_t)(P.K + 1) * 4, (void**)&bstart));
   ZK_TRY(ws.get("msm_sval", Mmax * 4, (void**)&sval));
   ZK_TRY(ws.get("msm_okey", Mmax * 4, (void**)&okey));
   ZK_TRY(ws.get("msm_oval", Mmax * 4, (void**)&oval));
@@ -1303,36 +1329,51 @@ static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, cons
   ZK_TRY(ws.get("msm_tstart", (size_t)(NH + 1) * 4, (void**)&tstart));
   ZK_TRY(ws.get("msm_bsums", ((std::max(len1, len2) + 1023) / 1024) * 4 + 16, (void**)&bsums));
   ZK_TRY(ws.get("msm_tot", 64, (void**)&tot));
-  ZK_TRY(ws.get("msm_buckets", (size_t)K * XW * 4, (void**)&buckets));
-  ZK_TRY(ws.get("msm_flags", 64 * 4, (void**)&flags));
-
-  // fork from the context stream (inputs ready); the context stream only
-  // waits for the digits pass, the one reader of the scalars
   ZK_HIP(hipEventRecord(lane->fork, ctx->stream));
   ZK_HIP(hipStreamWaitEvent(st, lane->fork, 0));
+  ScopedKernelTimer tm(ctx, "msm_sort", st);
+  ZK_TRY(dispatch_digits(P.c, st, d_scalars, n, P.p, P.W, digits));
+  ZK_HIP(hipEventRecord(lane->consumed, st));
+  ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
+  auto scan = [&](uint32_t* a, size_t len, uint32_t* total) {
+    uint32_t nb = (uint32_t)((len + 1023) / 1024);
+    k_scan_blocks<<<nb, 256, 0, st>>>(a, (uint32_t)len, a, bsums);
+    k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, total);
+    k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
+  };
+  const uint32_t ne = (uint32_t)P.ne;
+  k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, ne, P.B, NH, C1, nc1, cnt1);
+  scan(cnt1, len1, &tot[0]);
+  k_rs_p1_scatter<<<nc1, RS_THREADS, rs_scatter_lds(NH), st>>>(digits, Mmax, ne, P.B, NH, C1, nc1, cnt1, okey, oval);
+  k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, nc1, NH, &tot[0], C2, binstart, tstart);
+  ZK_HIP(hipMemsetAsync(cnt2, 0, len2 * 4, st));
+  k_rs_p2_count<<<T2max, RS_THREADS, 0, st>>>(okey, binstart, tstart, NH, C2, cnt2);
+  scan(cnt2, len2, &tot[1]);
+  k_rs_bstart<<<(P.K + 256) / 256, 256, 0, st>>>(cnt2, binstart, tstart, NH, P.K, bstart);
+  k_rs_p2_scatter<<<T2max, RS_THREADS, rs_scatter_lds(256), st>>>(okey, oval, binstart, tstart, NH, C2, cnt2, sval);
+  ZK_HIP(hipGetLastError());
+  *out_sval = sval;
+  *out_bstart = bstart;
+  return 0;
+}
+
+// Bucket accumulation + reduction of one base set over a sorted entry list,
+// on the lane stream; queues the D2H of the bit sums and the job's event.
+template <class G>
+static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const zkmi_bases* tb, size_t offset,
+                         size_t n, const uint32_t* sval, const uint32_t* bstart, zkmi_msm_job* job) {
+  constexpr int XW = 4 * G::CW;
+  hipStream_t st = lane->st;
+  Workspace& ws = lane->ws;
+  const uint32_t* d_bases = tb->d_pts + offset * G::PW;
+  const uint32_t K = P.K;
+  const int W = P.W, bb = P.bb, lb = P.lb, hb = P.hb;
+  const size_t Mmax = P.Mmax;
+  const uint32_t tn = (uint32_t)n, tskip = P.p > 1 ? (uint32_t)(tb->n - n) : 0u;
+  uint32_t *buckets, *flags;
+  ZK_TRY(ws.get("msm_buckets", (size_t)K * XW * 4, (void**)&buckets));
+  ZK_TRY(ws.get("msm_flags", 64 * 4, (void**)&flags));
   ZK_HIP(hipMemsetAsync(flags, 0, 64 * 4, st));
-  {
-    ScopedKernelTimer tm(ctx, "msm_sort", st);
-    ZK_TRY(dispatch_digits(c, st, d_scalars, d_bases, G::PW, n, p, W, digits));
-    ZK_HIP(hipEventRecord(lane->consumed, st));
-    ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
-    auto scan = [&](uint32_t* a, size_t len, uint32_t* total) {
-      uint32_t nb = (uint32_t)((len + 1023) / 1024);
-      k_scan_blocks<<<nb, 256, 0, st>>>(a, (uint32_t)len, a, bsums);
-      k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, total);
-      k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
-    };
-    k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, (uint32_t)ne, B, NH, C1, nc1, cnt1);
-    scan(cnt1, len1, &tot[0]);
-    k_rs_p1_scatter<<<nc1, RS_THREADS, rs_scatter_lds(NH), st>>>(digits, Mmax, (uint32_t)ne, B, NH, C1, nc1, cnt1, okey, oval);
-    k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, nc1, NH, &tot[0], C2, binstart, tstart);
-    ZK_HIP(hipMemsetAsync(cnt2, 0, len2 * 4, st));
-    k_rs_p2_count<<<T2max, RS_THREADS, 0, st>>>(okey, binstart, tstart, NH, C2, cnt2);
-    scan(cnt2, len2, &tot[1]);
-    k_rs_bstart<<<(K + 256) / 256, 256, 0, st>>>(cnt2, binstart, tstart, NH, K, bstart);
-    k_rs_p2_scatter<<<T2max, RS_THREADS, rs_scatter_lds(256), st>>>(okey, oval, binstart, tstart, NH, C2, cnt2, sval);
-    ZK_HIP(hipGetLastError());
-  }
   // level 0: fixed-size chunks of the sorted list (sized from the upper bound
   // W*n so no host round-trip is needed; chunks past M exit at once).
   // Threads per CU: measured best at ~1024 for G1 (over-subscribing the
@@ -1355,7 +1396,8 @@ static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, cons
   ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
   {
     ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
-    Acc0Kernel<G>::fn<<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, tn, tskip, buckets, xkey, xvalid, xpts);
+    Acc0Kernel<G>::fn<<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, tn, tskip, buckets, xkey,
+                                                          xvalid, xpts);
     ZK_HIP(hipGetLastError());
   }
   // segmented reduction of cut runs: level 1 pairs (tail, head) halves,
@@ -1401,18 +1443,83 @@ static int msm_submit_t(zkmi_ctx* ctx, const zkmi_bases* tb, size_t offset, cons
   return 0;
 }
 
-int msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
-               zkmi_msm_job** job) {
-  *job = nullptr;
+static int msm_acc_any(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const zkmi_bases* tb, size_t offset, size_t n,
+                       const uint32_t* sval, const uint32_t* bstart, zkmi_msm_job* job) {
+  return tb->g2 ? msm_acc_phase<G2T>(ctx, lane, P, tb, offset, n, sval, bstart, job)
+                : msm_acc_phase<G1T>(ctx, lane, P, tb, offset, n, sval, bstart, job);
+}
+
+static zkmi_msm_job* new_job(zkmi_ctx* ctx, const zkmi_bases* b, const MsmPlan& P, size_t n) {
+  return new zkmi_msm_job{ctx, b->g2, P.c, P.W, P.bb, nullptr, 0, nullptr, n == 0};
+}
+
+static int check_size(const MsmPlan& P, size_t n) {
+  if (P.ne >= (1u << 31) || P.Mmax >= (1ull << 32)) {
+    set_error("MSM size %zu too large for one call", n);
+    return ZKMI_EINVAL;
+  }
+  return 0;
+}
+
+#ifdef ZK_ACC0_TRACE
+extern "C" int zkmi_debug_acc0_trace(uint64_t* out, size_t nwaves) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zk_acc0_trace), nwaves * 32, 0, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  return 0;
+}
+#endif
+static int check_range(const zkmi_bases* b, size_t offset, size_t n) {
   if (!b || offset > b->n || n > b->n - offset) {
     set_error("msm: range [%zu, %zu) outside base set of %zu", offset, offset + n, b ? b->n : 0);
     return ZKMI_EINVAL;
   }
-  int rc = b->g2 ? msm_submit_t<G2T>(ctx, b, offset, (const uint32_t*)d_scalars, n, job)
-                 : msm_submit_t<G1T>(ctx, b, offset, (const uint32_t*)d_scalars, n, job);
-  if (rc != 0 && *job) {
-    msm_job_free(*job);
-    *job = nullptr;
+  return 0;
+}
+
+int msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+               zkmi_msm_job** job) {
+  zkmi_msm_job* jobs[1] = {nullptr};
+  int rc = msm_submit_shared(ctx, &b, 1, offset, d_scalars, n, jobs);
+  *job = jobs[0];
+  return rc;
+}
+
+// k MSMs with the same scalars (and range) over k base sets: one digits +
+// sort pass, then one accumulation per set, all on one lane.  Base sets whose
+// window plan differs from the first one's get their own sort.
+int msm_submit_shared(zkmi_ctx* ctx, const zkmi_bases* const* bs, int k, size_t offset, const void* d_scalars,
+                      size_t n, zkmi_msm_job** jobs) {
+  for (int i = 0; i < k; i++) jobs[i] = nullptr;
+  for (int i = 0; i < k; i++) ZK_TRY(check_range(bs[i], offset, n));
+  int rc = 0;
+  MsmLane* lane = nullptr;
+  std::vector<bool> done(k, false);
+  for (int i = 0; i < k && !rc; i++) {
+    if (done[i]) continue;
+    const MsmPlan P = msm_plan(ctx, bs[i], n);
+    jobs[i] = new_job(ctx, bs[i], P, n);
+    done[i] = true;
+    if (n == 0) {
+      for (int j = i + 1; j < k; j++)
+        if (!done[j]) jobs[j] = new_job(ctx, bs[j], msm_plan(ctx, bs[j], n), n), done[j] = true;
+      break;
+    }
+    if ((rc = check_size(P, n))) break;
+    if ((rc = get_lane(ctx, &lane))) break;
+    uint32_t *sval, *bstart;
+    if ((rc = msm_sort_phase(ctx, lane, P, (const uint32_t*)d_scalars, n, &sval, &bstart))) break;
+    if ((rc = msm_acc_any(ctx, lane, P, bs[i], offset, n, sval, bstart, jobs[i]))) break;
+    for (int j = i + 1; j < k && !rc; j++) {
+      if (done[j] || !same_plan(P, msm_plan(ctx, bs[j], n))) continue;
+      jobs[j] = new_job(ctx, bs[j], P, n);
+      done[j] = true;
+      rc = msm_acc_any(ctx, lane, P, bs[j], offset, n, sval, bstart, jobs[j]);
+    }
+  }
+  if (rc) {
+    for (int i = 0; i < k; i++) {
+      msm_job_free(jobs[i]);
+      jobs[i] = nullptr;
+    }
   }
   return rc;
 }

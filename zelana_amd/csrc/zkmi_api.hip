@@ -318,6 +318,14 @@ int zkmi_msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const voi
   return msm_submit(ctx, b, offset, d_scalars, n, job);
 }
 int zkmi_msm_wait(zkmi_msm_job* job, uint64_t* out_affine) { return msm_wait(job, out_affine); }
+int zkmi_msm_submit_shared(zkmi_ctx* ctx, const zkmi_bases* const* bs, int k, size_t offset, const void* d_scalars,
+                           size_t n, zkmi_msm_job** jobs) {
+  if (!ctx || !bs || !jobs || k < 1 || (n && !d_scalars)) {
+    set_error("zkmi_msm_submit_shared: bad arguments");
+    return ZKMI_EINVAL;
+  }
+  return msm_submit_shared(ctx, bs, k, offset, d_scalars, n, jobs);
+}
 int zkmi_msm_set_lanes(zkmi_ctx* ctx, int lanes) {
   if (!ctx || lanes < 1 || lanes > 8) {
     set_error("zkmi_msm_set_lanes: lanes must be in [1, 8]");

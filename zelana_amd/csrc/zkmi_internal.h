@@ -114,6 +114,10 @@ int msm_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_
 int msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                zkmi_msm_job** job);
 int msm_wait(zkmi_msm_job* job, uint64_t* out_affine);
+// k MSMs sharing scalars and range over k base sets (one sort when the window
+// plans agree); jobs[i] receives the job of bs[i]
+int msm_submit_shared(zkmi_ctx* ctx, const zkmi_bases* const* bs, int k, size_t offset, const void* d_scalars,
+                      size_t n, zkmi_msm_job** jobs);
 void msm_job_free(zkmi_msm_job* job);
 int bases_upload(zkmi_ctx* ctx, int g2, const uint64_t* host_affine, size_t n, zkmi_bases** out);
 // convert canonical affine already in device memory (n points) into a bases set

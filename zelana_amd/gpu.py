@@ -155,6 +155,14 @@ class Context:
         check(lib().zkmi_msm_submit(self.h, bases.h, offset, dscalars.ptr, n, ctypes.byref(job)), "zkmi_msm_submit")
         return (job, bases.g2)
 
+    def msm_submit_shared(self, bases_list, dscalars: DeviceBuffer, n: int, offset: int = 0):
+        """Queue MSMs of the same scalars over several base sets (one shared sort)."""
+        k = len(bases_list)
+        arr = (vp * k)(*[b.h for b in bases_list])
+        jobs = (vp * k)()
+        check(lib().zkmi_msm_submit_shared(self.h, arr, k, offset, dscalars.ptr, n, jobs), "zkmi_msm_submit_shared")
+        return [(vp(jobs[i]), b.g2) for i, b in enumerate(bases_list)]
+
     def msm_wait(self, job):
         h, g2 = job
         out = np.zeros(16 if g2 else 8, np.uint64)
