@@ -173,7 +173,8 @@ def test_msm_pipelined(ctx):
 
 
 # ---------------------------------------------------------- fixed-base tables
-@pytest.mark.parametrize("c,factor", [(0, 0), (8, 0), (11, 3), (13, 2), (16, 0), (17, 0), (17, 4), (6, 1)])
+@pytest.mark.parametrize("c,factor", [(0, 0), (8, 0), (11, 3), (13, 2), (16, 0), (17, 0), (17, 4), (6, 1),
+                                      (19, 0), (20, 0), (22, 0)])
 def test_msm_g1_table(ctx, c, factor):
     """MSM over a precomputed fixed-base table equals the plain MSM (oracle),
     for full and partial tables, offsets and infinity bases."""
@@ -192,7 +193,7 @@ def test_msm_g1_table(ctx, c, factor):
     sc = _rand_scalars(rng, 700)
     assert np.array_equal(ctx.msm(b, sc, offset=1234), O.msm_g1(pts[1234:1934], sc))
     # a pinned window different from the table's falls back to the plain path
-    other = 9 if info[1] != 9 else 10
+    other = 9 if info[1] != 9 else 10  # (pinned windows stay <= 17: plain path)
     ctx.set_window(other)
     try:
         assert np.array_equal(ctx.msm(b, sc, offset=5), O.msm_g1(pts[5:705], sc))
@@ -200,13 +201,13 @@ def test_msm_g1_table(ctx, c, factor):
         ctx.set_window(0)
 
 
-@pytest.mark.parametrize("factor", [0, 2])
-def test_msm_g2_table(ctx, factor):
+@pytest.mark.parametrize("c,factor", [(0, 0), (0, 2), (20, 0)])
+def test_msm_g2_table(ctx, c, factor):
     n = 1500
-    pts = O.gen_points_g2(4000 + factor, n)
+    pts = O.gen_points_g2(4000 + factor + c, n)
     pts[3] = 0
     b = ctx.bases_g2(pts)
-    b.precompute(0, factor)
+    b.precompute(c, factor)
     sc = _rand_scalars(np.random.default_rng(factor), n, "witness")
     assert np.array_equal(ctx.msm(b, sc), O.msm_g2(pts, sc))
     assert np.array_equal(ctx.msm(b, sc[:900], offset=600), O.msm_g2(pts[600:], sc[:900]))
@@ -254,3 +255,20 @@ def test_msm_shared_sort(ctx):
     assert np.array_equal(got[1], O.msm_g1(p2[2:n - 1], sc))
     assert np.array_equal(got[2], O.msm_g2(q2[2:n - 1], sc))
     assert np.array_equal(got[3], O.msm_g1(p2[2:n - 1], sc))
+
+
+def test_msm_items_path_2pow18(ctx):
+    """One-lane-per-bucket accumulation (table window 19 -> 2^18 buckets):
+    uniform and witness-like scalars (heavy buckets
+    split into pieces and merged by the segmented cascade)."""
+    n = 1 << 18
+    pts = O.gen_points_g1(1018, n, threads=16)
+    b = ctx.bases_g1(pts)
+    info = b.precompute(19, 0)
+    assert info[1] == 19
+    for kind, seed in (("uniform", 1), ("witness", 2)):
+        if kind == "uniform":
+            sc = O.gen_scalars(118, n)
+        else:
+            sc = _rand_scalars(np.random.default_rng(seed), n, "witness")
+        assert np.array_equal(ctx.msm(b, sc), O.msm_g1(pts, sc, threads=16)), kind

@@ -162,7 +162,6 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__
 // Only zero digits are dropped; order inside a bucket is irrelevant (group
 // addition is exact), so neither pass needs to be stable.
 constexpr int RS_THREADS = 256;
-constexpr uint32_t RS_LO = 8;
 
 __device__ __forceinline__ bool rs_key(const int32_t* __restrict__ digits, uint64_t e, uint32_t ne, uint32_t B,
                                        uint32_t& key, uint32_t& val) {
@@ -175,8 +174,8 @@ __device__ __forceinline__ bool rs_key(const int32_t* __restrict__ digits, uint6
 }
 
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_count(const int32_t* __restrict__ digits, uint64_t M, uint32_t ne,
-                                                            uint32_t B, uint32_t NH, uint32_t C1, uint32_t nc1,
-                                                            uint32_t* __restrict__ cnt1) {
+                                                            uint32_t B, uint32_t NH, uint32_t lob, uint32_t C1,
+                                                            uint32_t nc1, uint32_t* __restrict__ cnt1) {
   extern __shared__ uint32_t hist[];
   for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) hist[x] = 0;
   __syncthreads();
@@ -184,7 +183,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_count(const int32_t* __res
   for (uint32_t k = threadIdx.x; k < C1; k += RS_THREADS) {
     uint64_t e = base + k;
     uint32_t key, val;
-    if (e < M && rs_key(digits, e, ne, B, key, val)) atomicAdd(&hist[key >> RS_LO], 1u);
+    if (e < M && rs_key(digits, e, ne, B, key, val)) atomicAdd(&hist[key >> lob], 1u);
   }
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) cnt1[(size_t)x * nc1 + blockIdx.x] = hist[x];
@@ -274,15 +273,15 @@ __device__ __forceinline__ void rs_scatter_tiles(uint32_t count, uint32_t nb, ui
 __host__ __device__ constexpr size_t rs_scatter_lds(uint32_t nb) { return (3 * (size_t)nb + RS_THREADS + 2 * RS_ST) * 4; }
 
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_scatter(const int32_t* __restrict__ digits, uint64_t M,
-                                                              uint32_t ne, uint32_t B, uint32_t NH, uint32_t C1,
-                                                              uint32_t nc1, const uint32_t* __restrict__ offs1,
+                                                              uint32_t ne, uint32_t B, uint32_t NH, uint32_t lob,
+                                                              uint32_t C1, uint32_t nc1, const uint32_t* __restrict__ offs1,
                                                               uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
   extern __shared__ uint32_t lds[];
   for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) lds[2 * NH + x] = offs1[(size_t)x * nc1 + blockIdx.x];
   const uint64_t base = (uint64_t)blockIdx.x * C1;
   const uint32_t count = (uint32_t)std::min<uint64_t>(C1, M - base);
   auto load = [&](uint32_t e, uint32_t& key, uint32_t& val) { return rs_key(digits, base + e, ne, B, key, val); };
-  auto bin = [](uint32_t key) { return key >> RS_LO; };
+  auto bin = [lob](uint32_t key) { return key >> lob; };
   rs_scatter_tiles<decltype(load), decltype(bin), true>(count, NH, lds, load, bin, okey, oval);
 }
 
@@ -331,56 +330,70 @@ __device__ __forceinline__ uint32_t rs_tile_bin(const uint32_t* __restrict__ tst
   return lo;
 }
 
+// P2 tiles of one hi bin run on one XCD (workgroup i lands on XCD i % 8): the
+// bin's output range then stays in that XCD's L2 while its tiles scatter
+// short runs into it.  Tile of workgroup g: (g % 8) * per + g / 8.
+__device__ __forceinline__ uint32_t rs_xcd_tile(uint32_t g, uint32_t T2max) {
+  const uint32_t per = (T2max + 7) / 8;
+  return (g & 7) * per + (g >> 3);
+}
+
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p2_count(const uint32_t* __restrict__ okey,
                                                             const uint32_t* __restrict__ binstart,
                                                             const uint32_t* __restrict__ tstart, uint32_t NH,
-                                                            uint32_t C2, uint32_t* __restrict__ cnt2) {
-  __shared__ uint32_t hist[1u << RS_LO];
-  const uint32_t t = blockIdx.x;
+                                                            uint32_t lob, uint32_t C2, uint32_t T2max,
+                                                            uint32_t* __restrict__ cnt2) {
+  extern __shared__ uint32_t hist[];
+  const uint32_t NLO = 1u << lob, mask = NLO - 1;
+  const uint32_t t = rs_xcd_tile(blockIdx.x, T2max);
   if (t >= tstart[NH]) return;
   const uint32_t h = rs_tile_bin(tstart, NH, t), q = t - tstart[h], nt = tstart[h + 1] - tstart[h];
   const uint32_t lo = binstart[h] + q * C2, hi = min(lo + C2, binstart[h + 1]);
-  hist[threadIdx.x] = 0;
+  for (uint32_t x = threadIdx.x; x < NLO; x += RS_THREADS) hist[x] = 0;
   __syncthreads();
-  for (uint32_t p = lo + threadIdx.x; p < hi; p += RS_THREADS) atomicAdd(&hist[okey[p] & 255u], 1u);
+  for (uint32_t p = lo + threadIdx.x; p < hi; p += RS_THREADS) atomicAdd(&hist[okey[p] & mask], 1u);
   __syncthreads();
-  cnt2[(size_t)tstart[h] * 256 + (size_t)threadIdx.x * nt + q] = hist[threadIdx.x];
+  for (uint32_t x = threadIdx.x; x < NLO; x += RS_THREADS)
+    cnt2[((size_t)tstart[h] << lob) + (size_t)x * nt + q] = hist[x];
 }
 
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p2_scatter(const uint32_t* __restrict__ okey,
                                                               const uint32_t* __restrict__ oval,
                                                               const uint32_t* __restrict__ binstart,
                                                               const uint32_t* __restrict__ tstart, uint32_t NH,
-                                                              uint32_t C2, const uint32_t* __restrict__ offs2,
+                                                              uint32_t lob, uint32_t C2, uint32_t T2max,
+                                                              const uint32_t* __restrict__ offs2,
                                                               uint32_t* __restrict__ sval) {
   extern __shared__ uint32_t lds[];
-  const uint32_t t = blockIdx.x;
+  const uint32_t NLO = 1u << lob, mask = NLO - 1;
+  const uint32_t t = rs_xcd_tile(blockIdx.x, T2max);
   if (t >= tstart[NH]) return;
   const uint32_t h = rs_tile_bin(tstart, NH, t), q = t - tstart[h], nt = tstart[h + 1] - tstart[h];
   const uint32_t lo = binstart[h] + q * C2, hi = min(lo + C2, binstart[h + 1]);
-  lds[2 * 256 + threadIdx.x] = offs2[(size_t)tstart[h] * 256 + (size_t)threadIdx.x * nt + q];
+  for (uint32_t x = threadIdx.x; x < NLO; x += RS_THREADS)
+    lds[2 * NLO + x] = offs2[((size_t)tstart[h] << lob) + (size_t)x * nt + q];
   auto load = [&](uint32_t e, uint32_t& key, uint32_t& val) {
     key = okey[lo + e];
     val = oval[lo + e];
     return true;
   };
-  auto bin = [](uint32_t key) { return key & 255u; };
-  rs_scatter_tiles<decltype(load), decltype(bin), false>(hi - lo, 256, lds, load, bin, nullptr, sval);
+  auto bin = [mask](uint32_t key) { return key & mask; };
+  rs_scatter_tiles<decltype(load), decltype(bin), false>(hi - lo, NLO, lds, load, bin, nullptr, sval);
 }
 
 // bucket starts: start of key k = scanned count at (hi, lo, tile 0)
 __global__ void __launch_bounds__(256) k_rs_bstart(const uint32_t* __restrict__ offs2,
                                                    const uint32_t* __restrict__ binstart,
-                                                   const uint32_t* __restrict__ tstart, uint32_t NH, uint32_t K,
-                                                   uint32_t* __restrict__ bstart) {
+                                                   const uint32_t* __restrict__ tstart, uint32_t NH, uint32_t lob,
+                                                   uint32_t K, uint32_t* __restrict__ bstart) {
   uint32_t k = blockIdx.x * 256 + threadIdx.x;
   if (k > K) return;
   if (k == K) {
     bstart[K] = binstart[NH];
     return;
   }
-  uint32_t h = k >> RS_LO, lo = k & 255u, nt = tstart[h + 1] - tstart[h];
-  bstart[k] = nt ? offs2[(size_t)tstart[h] * 256 + (size_t)lo * nt] : binstart[h];
+  uint32_t h = k >> lob, lo = k & ((1u << lob) - 1), nt = tstart[h + 1] - tstart[h];
+  bstart[k] = nt ? offs2[((size_t)tstart[h] << lob) + (size_t)lo * nt] : binstart[h];
 }
 
 // ----------------------------------------------------------------- scan
@@ -679,6 +692,189 @@ struct Acc0Kernel<G2T> {
   static constexpr auto fn = k_msm_acc0_g2;
 };
 
+// ------------------------------------------------ one lane per bucket
+// For >= 2^18 buckets (fixed-base tables with c >= 19) the accumulation gives
+// each lane a whole bucket: no chunk edges, so no partial sums (except for
+// buckets longer than `cap`, split into cap-sized pieces), and no bucket
+// boundaries inside a lane's loop.  Work items are ordered by length,
+// longest first: the 64 lanes of a wave get equal trip counts and the waves
+// that run last are the shortest, so the tail is short.  (The chunked path
+// loses ~15% to its tail: resident waves of a SIMD finish in age order, the
+// last one alone and latency-bound; tools/trace_acc0.py.)
+constexpr uint32_t ITEM_CAP_MAX = 1024;
+constexpr uint32_t ITEMS_MIN_K = 1u << 18;
+constexpr uint32_t ITEM_SEQ_MAX = 32;  // pieces summed by one thread (k_items_combine)
+constexpr uint32_t NOSLOT = 0xFFFFFFFFu;
+
+__global__ void __launch_bounds__(256) k_items_count(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
+                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ hv,
+                                                     uint32_t* __restrict__ open_flag) {
+  __shared__ uint32_t lh[ITEM_CAP_MAX + 1];
+  for (uint32_t i = threadIdx.x; i <= cap; i += 256) lh[i] = 0;
+  __syncthreads();
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b < K) {
+    const uint32_t size = bstart[b + 1] - bstart[b];
+    const uint32_t np = (size + cap - 1) / cap;
+    if (size) {
+      if (np > 1) atomicAdd(&lh[cap], np - 1);
+      atomicAdd(&lh[size - (np - 1) * cap], 1u);
+    }
+    hv[b] = np > 1 ? np : 0;
+    if (np > ITEM_SEQ_MAX) atomicOr(open_flag, 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i <= cap; i += 256)
+    if (lh[i]) atomicAdd(&hist[i], lh[i]);
+}
+
+// one thread: cursors of the size classes, longest class first; total items
+__global__ void k_items_offsets(const uint32_t* __restrict__ hist, uint32_t cap, uint32_t* __restrict__ cursor,
+                                uint32_t* __restrict__ nitems) {
+  uint32_t run = 0;
+  for (uint32_t cl = cap; cl >= 1; cl--) {
+    cursor[cl] = run;
+    run += hist[cl];
+  }
+  *nitems = run;
+}
+
+__global__ void __launch_bounds__(256) k_items_scatter(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
+                                                       const uint32_t* __restrict__ pbase,
+                                                       uint32_t* __restrict__ cursor, uint4* __restrict__ items) {
+  __shared__ uint32_t lc[ITEM_CAP_MAX + 1], lbase[ITEM_CAP_MAX + 1];
+  for (uint32_t i = threadIdx.x; i <= cap; i += 256) lc[i] = 0;
+  __syncthreads();
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  uint32_t lo = 0, size = 0, np = 0, r_full = 0, r_last = 0, cl_last = 0;
+  if (b < K) {
+    lo = bstart[b];
+    size = bstart[b + 1] - lo;
+    np = (size + cap - 1) / cap;
+    if (size) {
+      if (np > 1) r_full = atomicAdd(&lc[cap], np - 1);
+      cl_last = size - (np - 1) * cap;
+      r_last = atomicAdd(&lc[cl_last], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i <= cap; i += 256) lbase[i] = lc[i] ? atomicAdd(&cursor[i], lc[i]) : 0;
+  __syncthreads();
+  if (b < K && size) {
+    const uint32_t pb = np > 1 ? pbase[b] : NOSLOT;
+    for (uint32_t q = 0; q + 1 < np; q++)
+      items[lbase[cap] + r_full + q] = make_uint4(lo + q * cap, lo + (q + 1) * cap, b, pb + q);
+    items[lbase[cl_last] + r_last] =
+        make_uint4(lo + (np - 1) * cap, lo + size, b, np > 1 ? pb + (np - 1) : NOSLOT);
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
+                                               const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
+                                               uint32_t tn, uint32_t tskip, uint32_t* __restrict__ buckets,
+                                               uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
+                                               uint32_t* __restrict__ xpts) {
+  using F = typename G::F;
+  constexpr int XW = 4 * G::CW;
+  constexpr int PQ = G::PW / 4;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *nitems) return;
+  const uint4 it = items[i];
+  const uint32_t start = it.x, end = it.y;
+  auto row = [&](uint32_t v) {
+    uint32_t idx = v & 0x7FFFFFFFu;
+    if (tskip) idx += (idx / tn) * tskip;
+    return reinterpret_cast<const uint4*>(bases + (size_t)idx * G::PW);
+  };
+  constexpr bool PF = G::CW == 8;  // G2: see msm_acc0_body
+  Xyzz<F> acc = xyzz_inf<F>();
+  uint32_t v_nxt = sval[start];
+  uint4 raw[PQ];
+  if constexpr (PF) {
+    const uint4* q = row(v_nxt);
+#pragma unroll
+    for (int k = 0; k < PQ; k++) raw[k] = q[k];
+  }
+  uint32_t v_nn = start + 1 < end ? sval[start + 1] : 0u;
+  for (uint32_t p = start; p < end; p++) {
+    uint4 cr[PQ];
+    const uint32_t v = v_nxt;
+    if constexpr (PF) {
+#pragma unroll
+      for (int k = 0; k < PQ; k++) cr[k] = raw[k];
+      if (p + 1 < end) {
+        const uint4* q = row(v_nn);
+#pragma unroll
+        for (int k = 0; k < PQ; k++) raw[k] = q[k];
+      }
+    } else {
+      const uint4* q = row(v);
+#pragma unroll
+      for (int k = 0; k < PQ; k++) cr[k] = q[k];
+    }
+    v_nxt = v_nn;
+    if (p + 2 < end) v_nn = sval[p + 2];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(cr);
+    if (w[G::PW - 1] >> 31) continue;  // base at infinity
+    Aff<F> P;
+    if constexpr (G::CW == 8) {
+      P.x = unpack(w);
+      P.y = fq_cneg(unpack(w + 8), v >> 31);
+      acc = xyzz_madd_g1(acc, P);
+    } else {
+      P.x = {unpack(w), unpack(w + 8)};
+      P.y = {fq_cneg(unpack(w + 16), v >> 31), fq_cneg(unpack(w + 24), v >> 31)};
+      acc = xyzz_madd_g2(acc, P);
+    }
+  }
+  if (it.w == NOSLOT) {
+    st_acc<G>(buckets + (size_t)it.z * XW, acc);
+  } else {
+    xkey[it.w] = it.z;
+    xvalid[it.w] = 1;
+    st_acc<G>(xpts + (size_t)it.w * XW, acc);
+  }
+}
+__global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
+    k_acc_items_g1(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
+                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
+                   uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
+                   uint32_t* __restrict__ xpts) {
+  acc_items_body<G1T>(items, nitems, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts);
+}
+__global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
+    k_acc_items_g2(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
+                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
+                   uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
+                   uint32_t* __restrict__ xpts) {
+  acc_items_body<G2T>(items, nitems, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts);
+}
+
+// Buckets split into 2..ITEM_SEQ_MAX pieces: one thread sums them (contiguous
+// partial slots) and invalidates them; longer ones stay for k_msm_accN.
+template <class G>
+__global__ void __launch_bounds__(256) k_items_combine(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
+                                                       const uint32_t* __restrict__ pbase,
+                                                       uint32_t* __restrict__ buckets, uint32_t* __restrict__ xvalid,
+                                                       const uint32_t* __restrict__ xpts) {
+  using F = typename G::F;
+  constexpr int XW = 4 * G::CW;
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= K) return;
+  const uint32_t size = bstart[b + 1] - bstart[b];
+  const uint32_t np = (size + cap - 1) / cap;
+  if (np < 2 || np > ITEM_SEQ_MAX) return;
+  const uint32_t s0 = pbase[b];
+  Xyzz<F> sum = ld_xyzz<G>(xpts + (size_t)s0 * XW);
+  xvalid[s0] = 0;
+  for (uint32_t q = 1; q < np; q++) {
+    sum = xyzz_add(sum, ld_xyzz<G>(xpts + (size_t)(s0 + q) * XW));
+    xvalid[s0 + q] = 0;
+  }
+  st_xyzz<G>(buckets + (size_t)b * XW, sum);
+}
+
 template <class G>
 __global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ xkey, const uint32_t* __restrict__ xvalid,
                                                   const uint32_t* __restrict__ xpts, uint32_t M, uint32_t L,
@@ -819,11 +1015,16 @@ __global__ void __launch_bounds__(256) k_msm_br(const uint32_t* __restrict__ src
       canon = true;
     }
   }
+  // every lane folds its strided share of the job's terms, then a 6-level LDS
+  // tree over the wave.  One curve-addition call site in one uniform loop (a
+  // second inlined copy spills G2); barriers only in the block-uniform tree
+  // steps.
+  const uint32_t nload = (1u << (lb > hb ? lb : hb)) / 64 + 1;
   Xyzz<F> v = xyzz_inf<F>();
-  for (int step = 0; step < 4 + 6; step++) {
+  for (uint32_t step = 0; step < nload + 6; step++) {
     Xyzz<F> q;
     bool act = false;
-    if (step < 4) {
+    if (step < nload) {
       uint32_t t = lane + 64u * step;
       if (live && t < cnt) {
         uint32_t e = BITS ? (bit < 0 ? t : insert_bit(t, bit)) : t * stride;
@@ -834,16 +1035,16 @@ __global__ void __launch_bounds__(256) k_msm_br(const uint32_t* __restrict__ src
         }
       }
     } else {
-      uint32_t sz = 32u >> (step - 4);
+      uint32_t sz = 32u >> (step - nload);
       if (lane >= sz && lane < 2 * sz) sh[wave][lane - sz] = v;
       __syncthreads();
       if (lane < sz) {
         q = sh[wave][lane];
-        act = true;
+        act = !xyzz_is_inf(q);
       }
     }
     if (act) v = xyzz_is_inf(v) ? q : xyzz_add(v, q);
-    if (step >= 4) __syncthreads();
+    if (step >= nload) __syncthreads();
   }
   if (live && lane == 0) {
     if (canon) {
@@ -1145,8 +1346,8 @@ int bases_upload(zkmi_ctx* ctx, int g2, const uint64_t* host_affine, size_t n, z
 }
 
 int bases_precompute(zkmi_bases* b, int c, int factor) {
-  if (c < 4 || c > 17) {
-    set_error("bases_precompute: window %d outside [4, 17]", c);
+  if (c < 4 || c > 22) {
+    set_error("bases_precompute: window %d outside [4, 22]", c);
     return ZKMI_EINVAL;
   }
   const int W = msm_windows(c);
@@ -1199,12 +1400,18 @@ int bases_precompute(zkmi_bases* b, int c, int factor) {
 }
 
 // Window for a full table over N bases: one window of W(c)*N entries and 2^(c-1)
-// buckets; bucket reduction costs ~3 additions per bucket.
+// buckets; bucket reduction costs ~2.5 additions per bucket.  From 2^18
+// buckets on, the accumulation runs one lane per bucket (k_acc_items).
 int table_window(size_t N) {
+  static const int env_c = [] {
+    const char* e = getenv("ZKMI_TABLE_C");  // experiments: pin the table window
+    return e ? atoi(e) : 0;
+  }();
+  if (env_c >= 4 && env_c <= 22) return env_c;
   int best = 8;
   double cost = 1e300;
-  for (int c = 6; c <= 17; c++) {
-    double k = (double)msm_windows(c) * (double)N + 3.0 * (double)(1u << (c - 1));
+  for (int c = 6; c <= 20; c++) {
+    double k = (double)msm_windows(c) * (double)N + 2.5 * (double)(1u << (c - 1));
     if (k < cost) {
       cost = k;
       best = c;
@@ -1232,7 +1439,7 @@ static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, size_t n, 
 #define ZK_C(CC) \
   case CC: launch_digits<CC>(st, sc, n, p, Wp, dg); break;
     ZK_C(4) ZK_C(5) ZK_C(6) ZK_C(7) ZK_C(8) ZK_C(9) ZK_C(10) ZK_C(11) ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15)
-    ZK_C(16) ZK_C(17)
+    ZK_C(16) ZK_C(17) ZK_C(18) ZK_C(19) ZK_C(20) ZK_C(21) ZK_C(22)
 #undef ZK_C
     default:
       set_error("unsupported MSM window %d", c);
@@ -1301,6 +1508,14 @@ static MsmPlan msm_plan(const zkmi_ctx* ctx, const zkmi_bases* tb, size_t n) {
 }
 static bool same_plan(const MsmPlan& a, const MsmPlan& b) { return a.c == b.c && a.p == b.p && a.W == b.W; }
 
+// exclusive scan of a[0..len) in place; *total = sum (bsums: len/1024 + 1 words)
+static void scan_excl(hipStream_t st, uint32_t* a, size_t len, uint32_t* bsums, uint32_t* total) {
+  uint32_t nb = (uint32_t)((len + 1023) / 1024);
+  k_scan_blocks<<<nb, 256, 0, st>>>(a, (uint32_t)len, a, bsums);
+  k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, total);
+  k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
+}
+
 // Digits + bucket sort on the lane stream: sval (sorted entries) and bstart
 // (K + 1 bucket starts) in the lane workspace.  The context stream waits only
 // for the digits pass, the one reader of the scalars.
@@ -1308,14 +1523,20 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
                           uint32_t** out_sval, uint32_t** out_bstart) {
   hipStream_t st = lane->st;
   Workspace& ws = lane->ws;
-  const uint32_t NH = (P.K + 255) >> RS_LO;
+  // hi digit = top 8 bits of the key (P1: <= 256 bins, long coalesced runs);
+  // lo digit = the rest (8..13 bits) inside each hi bin (P2, XCD-local)
+  uint32_t kb = 0;
+  while ((1u << kb) < P.K) kb++;
+  const uint32_t lob = kb > 16 ? kb - 8 : 8;
+  const uint32_t NH = (P.K + (1u << lob) - 1) >> lob;
   const size_t Mmax = P.Mmax;
   // radix-sort geometry (see k_rs_*): ~2K P1 chunks, ~8K P2 tiles at most
   const uint32_t C1 = 16384u * (uint32_t)std::max<size_t>(1, (Mmax + 16384ull * 2048 - 1) / (16384ull * 2048));
   const uint32_t nc1 = (uint32_t)((Mmax + C1 - 1) / C1);
-  const uint32_t C2 = 8192u * (uint32_t)std::max<size_t>(1, (Mmax + 8192ull * 8192 - 1) / (8192ull * 8192));
+  const uint32_t C2b = std::max(8192u, 4u << lob);  // >= 4 entries per lo bin per tile
+  const uint32_t C2 = C2b * (uint32_t)std::max<size_t>(1, (Mmax + (size_t)C2b * 8192 - 1) / ((size_t)C2b * 8192));
   const uint32_t T2max = (uint32_t)((Mmax + C2 - 1) / C2) + NH;
-  const size_t len1 = (size_t)NH * nc1, len2 = (size_t)T2max * 256;
+  const size_t len1 = (size_t)NH * nc1, len2 = (size_t)T2max << lob;
   int32_t* digits;
   uint32_t *bstart, *sval, *cnt1, *okey, *oval, *binstart, *tstart, *cnt2, *bsums, *tot;
   ZK_TRY(ws.get("msm_digits", Mmax * 4, (void**)&digits));
@@ -1342,15 +1563,18 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
     k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
   };
   const uint32_t ne = (uint32_t)P.ne;
-  k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, ne, P.B, NH, C1, nc1, cnt1);
+  k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1, cnt1);
   scan(cnt1, len1, &tot[0]);
-  k_rs_p1_scatter<<<nc1, RS_THREADS, rs_scatter_lds(NH), st>>>(digits, Mmax, ne, P.B, NH, C1, nc1, cnt1, okey, oval);
+  k_rs_p1_scatter<<<nc1, RS_THREADS, rs_scatter_lds(NH), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1, cnt1, okey,
+                                                                oval);
   k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, nc1, NH, &tot[0], C2, binstart, tstart);
   ZK_HIP(hipMemsetAsync(cnt2, 0, len2 * 4, st));
-  k_rs_p2_count<<<T2max, RS_THREADS, 0, st>>>(okey, binstart, tstart, NH, C2, cnt2);
+  const uint32_t g2 = ((T2max + 7) / 8) * 8;  // XCD-mapped grid (rs_xcd_tile)
+  k_rs_p2_count<<<g2, RS_THREADS, (1u << lob) * 4, st>>>(okey, binstart, tstart, NH, lob, C2, T2max, cnt2);
   scan(cnt2, len2, &tot[1]);
-  k_rs_bstart<<<(P.K + 256) / 256, 256, 0, st>>>(cnt2, binstart, tstart, NH, P.K, bstart);
-  k_rs_p2_scatter<<<T2max, RS_THREADS, rs_scatter_lds(256), st>>>(okey, oval, binstart, tstart, NH, C2, cnt2, sval);
+  k_rs_bstart<<<(P.K + 256) / 256, 256, 0, st>>>(cnt2, binstart, tstart, NH, lob, P.K, bstart);
+  k_rs_p2_scatter<<<g2, RS_THREADS, rs_scatter_lds(1u << lob), st>>>(okey, oval, binstart, tstart, NH, lob, C2, T2max,
+                                                                     cnt2, sval);
   ZK_HIP(hipGetLastError());
   *out_sval = sval;
   *out_bstart = bstart;
@@ -1374,38 +1598,80 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   ZK_TRY(ws.get("msm_buckets", (size_t)K * XW * 4, (void**)&buckets));
   ZK_TRY(ws.get("msm_flags", 64 * 4, (void**)&flags));
   ZK_HIP(hipMemsetAsync(flags, 0, 64 * 4, st));
-  // level 0: fixed-size chunks of the sorted list (sized from the upper bound
-  // W*n so no host round-trip is needed; chunks past M exit at once).
-  // Threads per CU: measured best at ~1024 for G1 (over-subscribing the
-  // resident waves evens out per-thread run lengths); ZKMI_ACC_TPC overrides.
-  static const size_t tpc_env = [] {
-    const char* e = getenv("ZKMI_ACC_TPC");
-    return e ? (size_t)atol(e) : (size_t)0;
-  }();
-  const size_t tpc = tpc_env ? tpc_env : 1024;
-  const size_t acc_threads = (size_t)ctx->num_cus * tpc;
-  uint32_t L = (uint32_t)std::max<size_t>(4, (Mmax + acc_threads - 1) / acc_threads);
-  uint32_t nch = (uint32_t)((Mmax + L - 1) / L);
   uint32_t *xkey, *xvalid, *xpts, *ykey, *yvalid, *ypts;
-  size_t xl = 2 * (size_t)nch + 1;
-  ZK_TRY(ws.get("msm_xkey", xl * 4 + 64, (void**)&xkey));
-  ZK_TRY(ws.get("msm_xvalid", xl * 4 + 64, (void**)&xvalid));
-  ZK_TRY(ws.get("msm_xpts", (xl + 2) * XW * 4, (void**)&xpts));
-  ZK_TRY(ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
-  ZK_TRY(ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
-  ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
-  {
+  size_t xl;  // length of the partial list the segmented cascade starts from
+  if (K >= ITEMS_MIN_K) {
+    // one lane per bucket (k_acc_items); partials only for buckets > cap
+    // Piece cap: no lane may run much longer than the kernel's share per
+    // resident lane (~M / (CUs x 768 lanes)), or its chain becomes the tail;
+    // buckets above it (low buckets that also take the short top window,
+    // witness-like 0/1 scalars) are split and their pieces summed after.
+    const size_t share = Mmax / ((size_t)ctx->num_cus * 768 * 2);
+    uint32_t cap = 64;
+    while (cap < share && cap < ITEM_CAP_MAX) cap <<= 1;
+    const size_t items_max = (size_t)K + (Mmax + cap - 1) / cap;
+    xl = 2 * ((Mmax + cap - 1) / cap) + 2;
+    uint32_t *hist, *cursor, *nitems, *hv, *bsums;
+    uint4* items;
+    ZK_TRY(ws.get("msm_it_hist", (ITEM_CAP_MAX + 1) * 4, (void**)&hist));
+    ZK_TRY(ws.get("msm_it_cursor", (ITEM_CAP_MAX + 1) * 4, (void**)&cursor));
+    ZK_TRY(ws.get("msm_it_n", 64, (void**)&nitems));
+    ZK_TRY(ws.get("msm_it_hv", ((size_t)K + 1) * 4, (void**)&hv));
+    ZK_TRY(ws.get("msm_it_bsums", ((size_t)K / 1024 + 2) * 4, (void**)&bsums));
+    ZK_TRY(ws.get("msm_items", items_max * 16, (void**)&items));
+    ZK_TRY(ws.get("msm_xkey", xl * 4 + 64, (void**)&xkey));
+    ZK_TRY(ws.get("msm_xvalid", xl * 4 + 64, (void**)&xvalid));
+    ZK_TRY(ws.get("msm_xpts", (xl + 2) * XW * 4, (void**)&xpts));
+    ZK_TRY(ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
+    ZK_TRY(ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
+    ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
     ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
-    Acc0Kernel<G>::fn<<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, tn, tskip, buckets, xkey,
-                                                          xvalid, xpts);
+    ZK_HIP(hipMemsetAsync(hist, 0, (ITEM_CAP_MAX + 1) * 4, st));
+    ZK_HIP(hipMemsetAsync(xkey, 0xFF, xl * 4, st));
+    ZK_HIP(hipMemsetAsync(xvalid, 0, xl * 4, st));
+    k_items_count<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hist, hv, &flags[0]);
+    scan_excl(st, hv, K, bsums, &nitems[1]);
+    k_items_offsets<<<1, 1, 0, st>>>(hist, cap, cursor, &nitems[0]);
+    k_items_scatter<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, cursor, items);
+    auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
+    kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, tn, tskip, buckets,
+                                                             xkey, xvalid, xpts);
+    k_items_combine<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, buckets, xvalid, xpts);
     ZK_HIP(hipGetLastError());
+  } else {
+    // level 0: fixed-size chunks of the sorted list (sized from the upper bound
+    // W*n so no host round-trip is needed; chunks past M exit at once).
+    // Threads per CU: measured best at ~1024 for G1 (over-subscribing the
+    // resident waves evens out per-thread run lengths); ZKMI_ACC_TPC overrides.
+    static const size_t tpc_env = [] {
+      const char* e = getenv("ZKMI_ACC_TPC");
+      return e ? (size_t)atol(e) : (size_t)0;
+    }();
+    const size_t tpc = tpc_env ? tpc_env : 1024;
+    const size_t acc_threads = (size_t)ctx->num_cus * tpc;
+    uint32_t L = (uint32_t)std::max<size_t>(4, (Mmax + acc_threads - 1) / acc_threads);
+    uint32_t nch = (uint32_t)((Mmax + L - 1) / L);
+    xl = 2 * (size_t)nch + 1;
+    ZK_TRY(ws.get("msm_xkey", xl * 4 + 64, (void**)&xkey));
+    ZK_TRY(ws.get("msm_xvalid", xl * 4 + 64, (void**)&xvalid));
+    ZK_TRY(ws.get("msm_xpts", (xl + 2) * XW * 4, (void**)&xpts));
+    ZK_TRY(ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
+    ZK_TRY(ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
+    ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
+    {
+      ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
+      Acc0Kernel<G>::fn<<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, tn, tskip, buckets, xkey,
+                                                            xvalid, xpts);
+      ZK_HIP(hipGetLastError());
+    }
+    ScopedKernelTimer tm(ctx, "msm_accN", st);
+    k_msm_cutsum<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, L, buckets, xvalid, xpts, &flags[0]);
   }
-  // segmented reduction of cut runs: level 1 pairs (tail, head) halves,
+  // segmented reduction of the remaining partials: level 1 pairs neighbours,
   // deeper levels only carry heavy buckets; each level exits on device when
   // the previous one left nothing open (no host round-trips)
   {
     ScopedKernelTimer tm(ctx, "msm_accN", st);
-    k_msm_cutsum<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, L, buckets, xvalid, xpts, &flags[0]);
     uint32_t cur_len = (uint32_t)xl;
     for (int level = 1; cur_len > 1; level++) {
       if (level >= 63) {
