@@ -965,51 +965,60 @@ __device__ __forceinline__ uint32_t insert_bit(uint32_t t, int bit) {
 }
 template <class G, bool BITS>
 __global__ void __launch_bounds__(256) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
-                                                const uint32_t* __restrict__ bstart, int lb, int hb, int W,
-                                                uint32_t* __restrict__ out0, uint32_t* __restrict__ out1) {
+                                                const uint32_t* __restrict__ bstart, int lb, int hb, int W, int sr,
+                                                int sc, int sb, uint32_t* __restrict__ out0,
+                                                uint32_t* __restrict__ out1) {
+  // Rows and columns are cut into sr / sc segments of <= 256 buckets, one wave
+  // each (enough waves for 2^19-bucket windows); C[h][seg], D[l][seg].  Bit
+  // sums are cut into sb segments of <= 256 terms; the host adds segments.
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   __shared__ Xyzz<F> sh[4][32];
   const int bb = lb + hb;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t job = blockIdx.x * 4 + wave;
-  const uint32_t njobs = BITS ? (uint32_t)W * (bb + 1) : (uint32_t)W * ((1u << hb) + (1u << lb));
+  const uint32_t nrow = ((uint32_t)W << hb) * sr, ncol = ((uint32_t)W << lb) * sc;
+  const uint32_t njobs = BITS ? (uint32_t)W * (bb + 1) * sb : nrow + ncol;
   const bool live = job < njobs;
   const uint32_t* src = src0;
-  uint32_t cnt = 0, stride = 1, bucket0 = 0;
-  int bit = -1;
+  uint32_t cnt = 0, stride = 1, bucket0 = 0, t0 = 0;
+  int bit = -1, seg = 1;
   uint32_t* dst = nullptr;
   bool canon = false;
   if (live) {
     if (!BITS) {
-      uint32_t nrow = (uint32_t)W << hb;
-      if (job < nrow) {  // row h of window w
-        uint32_t w = job >> hb, h = job & ((1u << hb) - 1);
-        bucket0 = (w << bb) + (h << lb);
-        cnt = 1u << lb;
+      if (job < nrow) {  // segment g of row h of window w
+        uint32_t rh = job / sr, g = job % sr, w = rh >> hb, h = rh & ((1u << hb) - 1);
+        cnt = (1u << lb) / sr;
+        bucket0 = (w << bb) + (h << lb) + g * cnt;
         stride = 1;
         dst = out0 + (size_t)job * XW;
-      } else {  // column l of window w
-        uint32_t jj = job - nrow, w = jj >> lb, l = jj & ((1u << lb) - 1);
-        bucket0 = (w << bb) + l;
-        cnt = 1u << hb;
+      } else {  // segment g of column l of window w
+        uint32_t jj = job - nrow, cl = jj / sc, g = jj % sc, w = cl >> lb, l = cl & ((1u << lb) - 1);
+        cnt = (1u << hb) / sc;
+        bucket0 = (w << bb) + ((g * cnt) << lb) + l;
         stride = 1u << lb;
         dst = out1 + (size_t)jj * XW;
       }
       src = src0 + (size_t)bucket0 * XW;
     } else {
-      uint32_t w = job / (bb + 1), j = job % (bb + 1);
-      if ((int)j < lb) {
-        src = src1 + ((size_t)w << lb) * XW;
-        cnt = 1u << (lb - 1);
+      const uint32_t wj = job / sb;
+      t0 = (job % sb) * 256u;  // this job's segment of the term range
+      uint32_t w = wj / (bb + 1), j = wj % (bb + 1);
+      if ((int)j < lb) {  // U_j over D[l][*] with bit j of l set
+        src = src1 + (((size_t)w << lb) * sc) * XW;
+        cnt = (1u << (lb - 1)) * sc;
         bit = (int)j;
-      } else if ((int)j < bb) {
-        src = src0 + ((size_t)w << hb) * XW;
-        cnt = 1u << (hb - 1);
+        seg = sc;
+      } else if ((int)j < bb) {  // U_j over C[h][*] with bit j - lb of h set
+        src = src0 + (((size_t)w << hb) * sr) * XW;
+        cnt = (1u << (hb - 1)) * sr;
         bit = (int)j - lb;
-      } else {
-        src = src0 + ((size_t)w << hb) * XW;
-        cnt = 1u << hb;
+        seg = sr;
+      } else {  // T = all C
+        src = src0 + (((size_t)w << hb) * sr) * XW;
+        cnt = (1u << hb) * sr;
+        seg = sr;
       }
       dst = out0 + (size_t)job * XW;
       canon = true;
@@ -1019,15 +1028,16 @@ __global__ void __launch_bounds__(256) k_msm_br(const uint32_t* __restrict__ src
   // tree over the wave.  One curve-addition call site in one uniform loop (a
   // second inlined copy spills G2); barriers only in the block-uniform tree
   // steps.
-  const uint32_t nload = (1u << (lb > hb ? lb : hb)) / 64 + 1;
+  const uint32_t nload = 256 / 64;
+  const uint32_t tend = BITS ? min(cnt, t0 + 256u) : cnt;
   Xyzz<F> v = xyzz_inf<F>();
   for (uint32_t step = 0; step < nload + 6; step++) {
     Xyzz<F> q;
     bool act = false;
     if (step < nload) {
-      uint32_t t = lane + 64u * step;
-      if (live && t < cnt) {
-        uint32_t e = BITS ? (bit < 0 ? t : insert_bit(t, bit)) : t * stride;
+      uint32_t t = t0 + lane + 64u * step;
+      if (live && t < tend) {
+        uint32_t e = BITS ? (bit < 0 ? t : insert_bit(t / seg, bit) * seg + t % seg) : t * stride;
         bool nonempty = BITS ? true : bstart[bucket0 + e + 1] > bstart[bucket0 + e];
         if (nonempty) {
           q = ld_xyzz<G>(src + (size_t)e * XW);
@@ -1456,10 +1466,11 @@ static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, size_t n, 
 struct zkmi_msm_job {
   zkmi_ctx* ctx;
   int g2, c, W, bb;
-  uint32_t* host;  // pinned: W*(bb+1) canonical XYZZ
+  uint32_t* host;  // pinned: W*(bb+1)*sb canonical XYZZ
   size_t host_words;
   hipEvent_t done;
   bool empty;
+  int sb = 1;  // segments per bit sum (added on the host)
 };
 
 namespace zk {
@@ -1691,17 +1702,22 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   }
   // bucket reduction -> W*(bb+1) canonical bit sums
   uint32_t *Cb, *Db, *sums;
-  ZK_TRY(ws.get("msm_C", (size_t)W * (1u << hb) * XW * 4, (void**)&Cb));
-  ZK_TRY(ws.get("msm_D", (size_t)W * (1u << lb) * XW * 4, (void**)&Db));
-  ZK_TRY(ws.get("msm_sums", (size_t)W * (bb + 1) * XW * 4, (void**)&sums));
+  const int sr = lb > 8 ? 1 << (lb - 8) : 1, sc = hb > 8 ? 1 << (hb - 8) : 1;  // <= 256 buckets per wave job
+  // bit-sum segments: the longest bit job sums max(2^hb * sr, 2^(lb-1) * sc) terms
+  const uint32_t maxterms = std::max((1u << hb) * sr, (1u << (lb - 1)) * sc);
+  const int sb = (int)((maxterms + 255) / 256);
+  ZK_TRY(ws.get("msm_C", (size_t)W * (1u << hb) * sr * XW * 4, (void**)&Cb));
+  ZK_TRY(ws.get("msm_D", (size_t)W * (1u << lb) * sc * XW * 4, (void**)&Db));
+  ZK_TRY(ws.get("msm_sums", (size_t)W * (bb + 1) * sb * XW * 4, (void**)&sums));
   {
     ScopedKernelTimer tm(ctx, "msm_bucket_reduce", st);
-    uint32_t jobs1 = (uint32_t)W * ((1u << hb) + (1u << lb)), jobs2 = (uint32_t)W * (bb + 1);
-    k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, st>>>(buckets, nullptr, bstart, lb, hb, W, Cb, Db);
-    k_msm_br<G, true><<<(jobs2 + 3) / 4, 256, 0, st>>>(Cb, Db, nullptr, lb, hb, W, sums, nullptr);
+    uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc)), jobs2 = (uint32_t)W * (bb + 1) * sb;
+    k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, st>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, Cb, Db);
+    k_msm_br<G, true><<<(jobs2 + 3) / 4, 256, 0, st>>>(Cb, Db, nullptr, lb, hb, W, sr, sc, sb, sums, nullptr);
     ZK_HIP(hipGetLastError());
   }
-  job->host_words = (size_t)W * (bb + 1) * XW;
+  job->sb = sb;
+  job->host_words = (size_t)W * (bb + 1) * sb * XW;
   ZK_TRY(ctx_pinned_get(ctx, job->host_words * 4, (void**)&job->host));
   ZK_HIP(hipMemcpyAsync(job->host, sums, job->host_words * 4, hipMemcpyDeviceToHost, st));
   ZK_HIP(hipEventCreateWithFlags(&job->done, hipEventDisableTiming));
@@ -1818,15 +1834,17 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
   int rc = timer_flush(ctx, false);
   auto th0 = std::chrono::steady_clock::now();
   // terms: V_{c w + j} = U_{w,j} (j < c-1), then T_w at weight 2^{c w}
-  int c = job->c, W = job->W, bb = job->bb, nbits = c * W;
-  std::vector<uint32_t> all((size_t)(nbits + W) * XW, 0);
+  // (each term arrives as sb segments, summed in the combine)
+  int c = job->c, W = job->W, bb = job->bb, nbits = c * W, sb = job->sb;
+  const size_t TW = (size_t)XW * sb;  // words per term
+  std::vector<uint32_t> all((size_t)(nbits + W) * TW, 0);
   for (int w = 0; w < W; w++) {
     for (int j = 0; j < bb; j++)
-      memcpy(&all[((size_t)c * w + j) * XW], &job->host[((size_t)w * (bb + 1) + j) * XW], XW * 4);
-    memcpy(&all[((size_t)nbits + w) * XW], &job->host[((size_t)w * (bb + 1) + bb) * XW], XW * 4);
+      memcpy(&all[((size_t)c * w + j) * TW], &job->host[((size_t)w * (bb + 1) + j) * TW], TW * 4);
+    memcpy(&all[((size_t)nbits + w) * TW], &job->host[((size_t)w * (bb + 1) + bb) * TW], TW * 4);
   }
-  if (!job->g2) msm_host_combine_g1(all.data(), nbits, W, c, out);
-  else msm_host_combine_g2(all.data(), nbits, W, c, out);
+  if (!job->g2) msm_host_combine_g1(all.data(), nbits, W, c, sb, out);
+  else msm_host_combine_g2(all.data(), nbits, W, c, sb, out);
   if (ctx->timer.enabled) {
     auto& t = ctx->timer.totals["msm_host_epilogue"];
     t.first += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();

@@ -65,14 +65,21 @@ void to_affine(const HX<F>& p, uint64_t* out) {
   put(out + K, F::mul(p.y, izzz));
 }
 
+// term k = sum of its `seg` segments (the GPU cuts long bit sums)
 template <class F, int CW>
-void combine(const uint32_t* terms, int nbits, int W, int c, uint64_t* out) {
+HX<F> ld_term_seg(const uint32_t* terms, size_t k, int seg) {
   constexpr int XW = 4 * CW;
+  HX<F> t = ld_term<F, CW>(terms + k * seg * XW);
+  for (int s = 1; s < seg; s++) t = zk::xyzz_add(t, ld_term<F, CW>(terms + (k * seg + s) * XW));
+  return t;
+}
+template <class F, int CW>
+void combine(const uint32_t* terms, int nbits, int W, int c, int seg, uint64_t* out) {
   HX<F> acc = zk::xyzz_inf<F>();
   for (int k = nbits - 1; k >= 0; k--) {
     acc = zk::xyzz_dbl(acc);
-    acc = zk::xyzz_add(acc, ld_term<F, CW>(terms + (size_t)k * XW));
-    if (k % c == 0) acc = zk::xyzz_add(acc, ld_term<F, CW>(terms + (size_t)(nbits + k / c) * XW));
+    acc = zk::xyzz_add(acc, ld_term_seg<F, CW>(terms, (size_t)k, seg));
+    if (k % c == 0) acc = zk::xyzz_add(acc, ld_term_seg<F, CW>(terms, (size_t)(nbits + k / c), seg));
   }
   (void)W;
   to_affine<F, CW>(acc, out);
@@ -99,11 +106,11 @@ HX<F> from_aff_canon(const uint64_t* a) {
 }  // namespace
 
 namespace zk {
-void msm_host_combine_g1(const uint32_t* terms, int nbits, int W, int c, uint64_t out[8]) {
-  combine<HFq, 8>(terms, nbits, W, c, out);
+void msm_host_combine_g1(const uint32_t* terms, int nbits, int W, int c, int seg, uint64_t out[8]) {
+  combine<HFq, 8>(terms, nbits, W, c, seg, out);
 }
-void msm_host_combine_g2(const uint32_t* terms, int nbits, int W, int c, uint64_t out[16]) {
-  combine<HFq2, 16>(terms, nbits, W, c, out);
+void msm_host_combine_g2(const uint32_t* terms, int nbits, int W, int c, int seg, uint64_t out[16]) {
+  combine<HFq2, 16>(terms, nbits, W, c, seg, out);
 }
 void host_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {
   auto r = xyzz_add(from_aff_canon<HFq, 4>(a), from_aff_canon<HFq, 4>(b));

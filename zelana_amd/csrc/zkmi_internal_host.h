@@ -7,8 +7,8 @@ namespace zk {
 // MSM epilogue: terms[k] (k < nbits) = canonical packed XYZZ of weight 2^k;
 // terms[nbits + w] (w < W) = window total T_w of weight 2^(c w).  Result is
 // canonical affine (all-zero = infinity).
-void msm_host_combine_g1(const uint32_t* terms, int nbits, int W, int c, uint64_t out[8]);
-void msm_host_combine_g2(const uint32_t* terms, int nbits, int W, int c, uint64_t out[16]);
+void msm_host_combine_g1(const uint32_t* terms, int nbits, int W, int c, int seg, uint64_t out[8]);
+void msm_host_combine_g2(const uint32_t* terms, int nbits, int W, int c, int seg, uint64_t out[16]);
 void host_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
 void host_g2_add_affine(const uint64_t a[16], const uint64_t b[16], uint64_t out[16]);
 // arkworks compressed encodings and the Solana 256-byte proof layout
