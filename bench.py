@@ -121,7 +121,7 @@ def main():
 
     def stages(k):
         out = {}
-        for name in ("msm_sort", "msm_acc0_g1", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"):
+        for name in ("msm_sort", "msm_items_plan", "msm_acc0_g1", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"):
             t, c = ctx.profile_get(name)
             if c:
                 out[name] = round(t / k, 4)
@@ -183,7 +183,10 @@ def main():
         rate = pmc["sq_insts_valu"] / kavg_s
         valu = {"bound": "valu", "achieved": round(rate / 1e9, 1), "peak": VALU_PEAK_G, "unit": "G wave-instr/s",
                 "frac": round(rate / 1e9 / VALU_PEAK_G, 4), "sq_insts_valu_per_launch": pmc["sq_insts_valu"],
-                "note": "the bound that applies: 256 CU x 4 SIMD x 2.4 GHz / 4 cycles per wave64 integer VALU op"}
+                "note": "the bound that applies: peak = 256 CU x 4 SIMD x 2.4 GHz / 4 cycles per wave64 VALU op "
+                        "(v_mad_u64_u32, which dominates, measured at that rate; gfx950 issues 32-bit ops in 2 "
+                        "cycles and clocks ~2.0 GHz under this load, see DESIGN.md); instructions from the "
+                        "committed profiles/pmc_traffic.json"}
     line = {
         "metric": "BN254 G1 MSM Mpoint-scalar/s + L2 proofs/sec at 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -305,7 +308,7 @@ def bench_l2(ctx, log_n, steps):
         dt = (time.perf_counter() - t0) / steps
         ctx.profile(False)
         st = {}
-        for k in ("g16_matvec", "g16_scale", "g16_qap", "ntt_group", "ntt_small", "msm_sort", "msm_acc0_g1",
+        for k in ("g16_matvec", "g16_scale", "g16_qap", "ntt_group", "ntt_small", "msm_sort", "msm_items_plan", "msm_acc0_g1",
                   "msm_acc0_g2", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"):
             t, c = ctx.profile_get(k)
             if c:

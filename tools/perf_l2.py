@@ -31,7 +31,7 @@ for lanes in (1, 2):
     dt = (time.perf_counter() - t0) / steps
     ctx.profile(False)
     print(f"lanes={lanes}: {dt*1e3:.2f} ms/proof -> {1/dt:.2f} proofs/s", flush=True)
-    for k in ("g16_matvec", "g16_scale", "g16_qap", "ntt_group", "ntt_small", "ntt_bitrev", "msm_sort", "msm_acc0_g1",
+    for k in ("g16_matvec", "g16_scale", "g16_qap", "ntt_group", "ntt_small", "ntt_bitrev", "msm_sort", "msm_items_plan", "msm_acc0_g1",
               "msm_acc0_g2", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue", "g16_witness_map", "g16_total"):
         t, c = ctx.profile_get(k)
         if c:

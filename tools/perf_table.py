@@ -40,7 +40,7 @@ for cfg, nl in [(c, nl) for c in cfgs for nl in lanes]:
     ctx.profile(False)
     print(f"{cfg} lanes={nl}: 2^{log_n} {'G2' if g2 else 'G1'} pipelined {dt*1e3:.3f} ms -> {n/dt/1e6:.1f} Mpt/s "
           f"same={np.array_equal(r, ref) and np.array_equal(r2, ref)}", flush=True)
-    for k in ["msm_sort", "msm_acc0_g1", "msm_acc0_g2", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"]:
+    for k in ["msm_sort", "msm_items_plan", "msm_acc0_g1", "msm_acc0_g2", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"]:
         t, cnt = ctx.profile_get(k)
         if cnt:
             print(f"   {k:20s} {t/K:8.3f} ms/step")

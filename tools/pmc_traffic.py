@@ -18,7 +18,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KMAP = {"msm_acc0_g1": "k_msm_acc0_g1", "msm_acc0_g2": "k_msm_acc0_g2"}
+KMAP = {"msm_acc0_g1": ("k_msm_acc0_g1", "k_acc_items_g1"), "msm_acc0_g2": ("k_msm_acc0_g2", "k_acc_items_g2")}
 
 
 def per_launch(d, counter, sym):
@@ -28,7 +28,7 @@ def per_launch(d, counter, sym):
     vals = {}
     with open(files[0]) as f:
         for r in csv.DictReader(f):
-            if sym in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if any(x in r["Kernel_Name"] for x in sym) and r["Counter_Name"] == counter:
                 key = r.get("Dispatch_Id") or r.get("Correlation_Id")
                 vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
     if not vals:

@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-KMAP = {"msm_acc0_g1": "k_msm_acc0_g1", "msm_acc0_g2": "k_msm_acc0_g2"}
+KMAP = {"msm_acc0_g1": ("k_msm_acc0_g1", "k_acc_items_g1"), "msm_acc0_g2": ("k_msm_acc0_g2", "k_acc_items_g2")}
 
 
 def main():
@@ -36,7 +36,7 @@ def main():
         with open(trace[0]) as f:
             rows = list(csv.DictReader(f))
         sym = KMAP.get(rf["kernel"], rf["kernel"])
-        ks = sorted((r for r in rows if sym in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
+        ks = sorted((r for r in rows if any(x in r["Kernel_Name"] for x in sym)), key=lambda r: int(r["Start_Timestamp"]))
         first, count = rf["kernel_launches"]["first"], rf["kernel_launches"]["count"]
         sel = ks[first:first + count]
         if sel:

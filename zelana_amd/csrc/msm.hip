@@ -1611,7 +1611,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   ZK_HIP(hipMemsetAsync(flags, 0, 64 * 4, st));
   uint32_t *xkey, *xvalid, *xpts, *ykey, *yvalid, *ypts;
   size_t xl;  // length of the partial list the segmented cascade starts from
-  if (K >= ITEMS_MIN_K) {
+  if (K >= ITEMS_MIN_K && W <= 2) {  // table plans (one window of many buckets)
     // one lane per bucket (k_acc_items); partials only for buckets > cap
     // Piece cap: no lane may run much longer than the kernel's share per
     // resident lane (~M / (CUs x 768 lanes)), or its chain becomes the tail;
@@ -1636,17 +1636,23 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     ZK_TRY(ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
     ZK_TRY(ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
     ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
-    ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
-    ZK_HIP(hipMemsetAsync(hist, 0, (ITEM_CAP_MAX + 1) * 4, st));
-    ZK_HIP(hipMemsetAsync(xkey, 0xFF, xl * 4, st));
-    ZK_HIP(hipMemsetAsync(xvalid, 0, xl * 4, st));
-    k_items_count<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hist, hv, &flags[0]);
-    scan_excl(st, hv, K, bsums, &nitems[1]);
-    k_items_offsets<<<1, 1, 0, st>>>(hist, cap, cursor, &nitems[0]);
-    k_items_scatter<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, cursor, items);
-    auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
-    kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, tn, tskip, buckets,
-                                                             xkey, xvalid, xpts);
+    {
+      ScopedKernelTimer tm(ctx, "msm_items_plan", st);
+      ZK_HIP(hipMemsetAsync(hist, 0, (ITEM_CAP_MAX + 1) * 4, st));
+      ZK_HIP(hipMemsetAsync(xkey, 0xFF, xl * 4, st));
+      ZK_HIP(hipMemsetAsync(xvalid, 0, xl * 4, st));
+      k_items_count<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hist, hv, &flags[0]);
+      scan_excl(st, hv, K, bsums, &nitems[1]);
+      k_items_offsets<<<1, 1, 0, st>>>(hist, cap, cursor, &nitems[0]);
+      k_items_scatter<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, cursor, items);
+    }
+    {
+      ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
+      auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
+      kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, tn, tskip, buckets,
+                                                               xkey, xvalid, xpts);
+    }
+    ScopedKernelTimer tm(ctx, "msm_accN", st);
     k_items_combine<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, buckets, xvalid, xpts);
     ZK_HIP(hipGetLastError());
   } else {
