@@ -113,6 +113,25 @@ int oracle_witness_map(const oracle_r1cs* cs, const uint64_t* zc, uint64_t* h, i
   return 0;
 }
 
+/* first constraint i with <A_i,z> * <B_i,z> != <C_i,z>, or -1 (test helper) */
+long long oracle_r1cs_check(const oracle_r1cs* cs, const uint64_t* zc) {
+  oracle_init();
+  size_t nv = cs->num_instance + cs->num_witness;
+  fe* z = (fe*)malloc(nv * sizeof(fe));
+  for (size_t i = 0; i < nv; i++) fe_from_canon(&FR, &z[i], zc + 4 * i);
+  long long bad = -1;
+  for (size_t i = 0; i < cs->num_constraints && bad < 0; i++) {
+    fe a, b, c, ab;
+    eval_row(&a, cs->a_rowptr, cs->a_col, cs->a_val, i, z);
+    eval_row(&b, cs->b_rowptr, cs->b_col, cs->b_val, i, z);
+    eval_row(&c, cs->c_rowptr, cs->c_col, cs->c_val, i, z);
+    fe_mul(&FR, &ab, &a, &b);
+    if (!fe_eq(&ab, &c)) bad = (long long)i;
+  }
+  free(z);
+  return bad;
+}
+
 /* ------------------------------------------------ fixed-base scalar mults */
 /* table[i][j] = j * 2^(8i) * G (affine), 32 x 256 */
 typedef struct { g1a* t1; g2a* t2; } fb_table;

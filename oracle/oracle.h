@@ -184,6 +184,8 @@ int oracle_groth16_prove(const void* pk, const oracle_r1cs* cs, const uint64_t* 
                          void* rng, const uint64_t* rs /* 8 u64 or NULL */,
                          int nthreads, uint64_t out_a[8], uint64_t out_b[16],
                          uint64_t out_c[8], uint64_t* out_h /* n canon or NULL */);
+/* first unsatisfied constraint index, or -1 */
+long long oracle_r1cs_check(const oracle_r1cs* cs, const uint64_t* z);
 /* witness_map only: h (n canonical values) */
 int oracle_witness_map(const oracle_r1cs* cs, const uint64_t* z, uint64_t* h,
                        int nthreads);

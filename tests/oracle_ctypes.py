@@ -57,6 +57,8 @@ def lib():
         L.oracle_vk_serialize.argtypes = [vp, ctypes.c_int, u8p, ctypes.c_size_t]
         L.oracle_groth16_prove.argtypes = [vp, vp, u64p, vp, u64p, ctypes.c_int, u64p, u64p, u64p, u64p]
         L.oracle_witness_map.argtypes = [vp, u64p, u64p, ctypes.c_int]
+        L.oracle_r1cs_check.restype = ctypes.c_longlong
+        L.oracle_r1cs_check.argtypes = [vp, u64p]
         L.oracle_pk_get.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, u64p]
         L.oracle_g1_serialize.argtypes = [u64p, ctypes.c_int, u8p]
         L.oracle_g2_serialize.argtypes = [u64p, ctypes.c_int, u8p]

@@ -1,0 +1,72 @@
+"""GPU Groth16 on the zelana_batch circuit (config 4's workload): reduced
+synthetic batches proved on the GPU equal the oracle's proofs (key from the
+oracle's setup, r and s from StdRng::seed_from_u64(batch_id) as
+prover.rs:354); on the full batch-70 circuit (2^21 domain) the GPU witness
+map equals the oracle's."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+from zelana_amd import zbatch as Z
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from zelana_amd.gpu import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _oracle_prove(opk, st, z, r, s):
+    a, b, c = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+    rs = np.concatenate([O.int_to_limbs(r), O.int_to_limbs(s)])
+    assert O.lib().oracle_groth16_prove(opk, ctypes.byref(st), O.P(z), None, O.P(rs), 8,
+                                        O.P(a), O.P(b), O.P(c), None) == 0
+    return a, b, c
+
+
+@pytest.mark.parametrize("depth,ntx", [(2, 1), (3, 2)])
+def test_zbatch_reduced_proof_matches_oracle(ctx, depth, ntx):
+    from zelana_amd import gpu
+    from zelana_amd.rng import StdRng
+    d = Z.synthetic_batch(depth, ntx, seed=100 + depth)
+    cs, z, _ = Z.build(d, max_transfers=ntx, max_withdrawals=1, max_shielded=1, depth=depth)
+    st, keep = O.make_r1cs(cs)
+    assert O.lib().oracle_r1cs_check(ctypes.byref(st), O.P(z)) == -1
+    rng = O.Rng(0)  # keygen seed 0
+    opk = O.lib().oracle_groth16_setup(ctypes.byref(st), rng.h, 8)
+    size = O.lib().oracle_pk_serialize(opk, 1, None, 0)
+    buf = np.zeros(size, np.uint8)
+    O.lib().oracle_pk_serialize(opk, 1, buf.ctypes.data, size)
+    pk = gpu.ProvingKey(ctx, buf.tobytes(), True)
+    prs = StdRng.seed_from_u64(int(d["batch_id"]))
+    r, s = prs.fr_rand(), prs.fr_rand()
+    want = _oracle_prove(opk, st, z, r, s)
+    got = gpu.groth16_prove(ctx, pk, cs, z, r, s)
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+    pk.precompute()
+    for g, w in zip(gpu.groth16_prove(ctx, pk, cs, z, r, s), want):
+        assert np.array_equal(g, w)
+    O.lib().oracle_pk_free(opk)
+
+
+def test_zbatch_batch70_witness_map(ctx):
+    from zelana_amd import gpu
+    d = Z.load_prover_toml(os.path.join(GOLD, "zelana_batch_70_Prover.toml"))
+    cs, z, _ = Z.build(d)
+    n = 1
+    while n < cs.num_constraints + cs.num_instance:
+        n <<= 1
+    assert n == 1 << 21
+    st, keep = O.make_r1cs(cs)
+    want = np.zeros((n, 4), np.uint64)
+    O.lib().oracle_witness_map(ctypes.byref(st), O.P(z), O.P(want), 16)
+    assert np.array_equal(gpu.witness_map(ctx, cs, z), want)

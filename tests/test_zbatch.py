@@ -1,0 +1,84 @@
+"""zelana_batch front-end (zelana_amd/zbatch.py) on CPU: MiMC against the
+reference's own known answers, the full batch-70 circuit against
+forge/circuits/zelana_batch/Prover.toml (a committed copy of its public inputs
+and witness is in tests/golden/), R1CS satisfaction through the oracle."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+from zelana_amd import zbatch as Z
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _batch70():
+    return Z.load_prover_toml(os.path.join(GOLD, "zelana_batch_70_Prover.toml"))
+
+
+def test_mimc_round_constants_and_kat58():
+    # mimc.rs:300-312 (round constants) and the batch-58 batch hash (mimc.rs:386-450)
+    assert Z.RC[:3] == [2, 10, 30]
+    nul = 7616971353247117454465635208226161158442151985157735778832845157632758123933
+    cm = 9742579207011299985260428178793458874858518230054558356243537317566210478598
+    assert Z.batch_hash_host(58, shielded=[(nul, cm)]) == \
+        1763393191922739858634693308814702990929063366376880176226696705996392451429
+
+
+def test_batch70_host_recompute():
+    """Sequential Merkle updates of the 5 transfers reproduce post_state_root;
+    batch hash and withdrawal root reproduce the file's public inputs."""
+    d = _batch70()
+    root = int(d["pre_state_root"])
+    txs = []
+    for t in d["transfers"]:
+        if not t["is_valid"]:
+            continue
+        spk, sbal, sn, amt = (int(t[k]) for k in ("sender_pubkey", "sender_balance", "sender_nonce", "amount"))
+        rpk, rbal, rn = (int(t[k]) for k in ("receiver_pubkey", "receiver_balance", "receiver_nonce"))
+        sp, si = [int(x) for x in t["sender_path"]], [int(x) for x in t["sender_path_indices"]]
+        rp, ri = [int(x) for x in t["receiver_path"]], [int(x) for x in t["receiver_path_indices"]]
+        assert Z.merkle_root(Z.account_leaf(spk, sbal, sn), sp, si) == root
+        root = Z.merkle_root(Z.account_leaf(spk, sbal - amt, sn + 1), sp, si)
+        assert Z.merkle_root(Z.account_leaf(rpk, rbal, rn), rp, ri) == root
+        root = Z.merkle_root(Z.account_leaf(rpk, rbal + amt, rn), rp, ri)
+        txs.append((spk, rpk, amt, sn))
+    assert root == int(d["post_state_root"])
+    bid = int(d["batch_id"])
+    assert Z.batch_hash_host(bid, transfers=txs) == int(d["batch_hash"])
+    assert Z.mimc_hash(Z.mimc_hash(5, bid), 0) == int(d["withdrawal_root"])
+
+
+def test_batch70_circuit_satisfied():
+    d = _batch70()
+    cs, z, computed = Z.build(d)
+    for k in Z.PUBLIC:
+        assert computed[k] == int(d[k]) % Z.R, k
+    assert cs.num_instance == 8 and cs.num_constraints > 1_000_000
+    st, keep = O.make_r1cs(cs)
+    assert O.lib().oracle_r1cs_check(ctypes.byref(st), O.P(z)) == -1
+    # any single witness change breaks it (an input, a MiMC round value, a bit)
+    for i in (9, 5000, cs.num_variables - 3):
+        z2 = z.copy()
+        z2[i, 0] ^= 1
+        assert O.lib().oracle_r1cs_check(ctypes.byref(st), O.P(z2)) >= 0
+
+
+def test_batch70_wrong_public_input_unsatisfied():
+    d = _batch70()
+    d["post_state_root"] = str(int(d["post_state_root"]) + 1)
+    cs, z, _ = Z.build(d)
+    st, keep = O.make_r1cs(cs)
+    assert O.lib().oracle_r1cs_check(ctypes.byref(st), O.P(z)) >= 0
+
+
+@pytest.mark.parametrize("depth,ntx", [(2, 1), (4, 3)])
+def test_synthetic_batches(depth, ntx):
+    d = Z.synthetic_batch(depth, ntx, seed=depth * 10 + ntx)
+    cs, z, computed = Z.build(d, max_transfers=ntx, max_withdrawals=1, max_shielded=1, depth=depth)
+    for k in Z.PUBLIC:
+        assert computed[k] == d[k] % Z.R, k
+    st, keep = O.make_r1cs(cs)
+    assert O.lib().oracle_r1cs_check(ctypes.byref(st), O.P(z)) == -1
