@@ -318,23 +318,18 @@ __global__ void k_domain_consts(uint32_t logn, uint32_t* __restrict__ out) {
 static const uint32_t G5[8] = {5, 0, 0, 0, 0, 0, 0, 0};
 static const uint32_t GINV5[8] = {0xc6666667u, 0xe7f3fbd4u, 0xca4a2d06u, 0xa9ae5ce9u,
                                   0x33cd568bu, 0x49b9b57cu, 0x5a13d9aau, 0x135b5294u};
-constexpr uint32_t COSET_KB = 14;
-
 // per-log_n constants and coset power tables, cached in the context
-struct DomainCache {
-  uint32_t* consts;  // [n^-1 canon | vinv mont]
-  uint32_t *lo_g, *hi_g, *lo_gi, *hi_gi;
-};
-static int domain_cache(zkmi_ctx* ctx, uint32_t logn, DomainCache* dc) {
+int domain_cache(zkmi_ctx* ctx, uint32_t logn, DomainCache* dc) {
   char nm[64];
   snprintf(nm, sizeof(nm), "g16_consts_%u", logn);
   bool fresh = ctx->ws.bufs.find(nm) == ctx->ws.bufs.end();
-  ZK_TRY(ctx->ws.get(nm, 64, (void**)&dc->consts));
+  ZK_TRY(ctx->ws.get(nm, 96, (void**)&dc->consts));
+  dc->ninv_m = dc->consts + 16;
   uint32_t nhi = std::max<uint32_t>(1, (uint32_t)(((1ull << logn) + (1u << COSET_KB) - 1) >> COSET_KB));
   uint32_t nlo = 1u << COSET_KB;
-  const char* names[4] = {"lo_g", "hi_g", "lo_gi", "hi_gi"};
-  uint32_t** ptrs[4] = {&dc->lo_g, &dc->hi_g, &dc->lo_gi, &dc->hi_gi};
-  for (int t = 0; t < 4; t++) {
+  const char* names[5] = {"lo_g", "hi_g", "lo_gi", "hi_gi", "hi_gf"};
+  uint32_t** ptrs[5] = {&dc->lo_g, &dc->hi_g, &dc->lo_gi, &dc->hi_gi, &dc->hi_gf};
+  for (int t = 0; t < 5; t++) {
     char tn[64];
     snprintf(tn, sizeof(tn), "g16_%s_%u", names[t], logn);
     ZK_TRY(ctx->ws.get(tn, (size_t)((t & 1) ? nhi : nlo) * 32, (void**)ptrs[t]));
@@ -350,14 +345,14 @@ static int domain_cache(zkmi_ctx* ctx, uint32_t logn, DomainCache* dc) {
     // n^-1 as a Montgomery multiplier for the hi tables: convert via a tiny
     // table build with step 0 (tab[x] = n^-1 * base^0) is avoided: fold it in
     // through mult_m = Montgomery(n^-1) computed by k_to_mont_fr.
-    uint32_t* ninv_m;
-    ZK_TRY(ctx->ws.get("g16_ninv_m", 32, (void**)&ninv_m));
+    uint32_t* ninv_m = dc->ninv_m;
     k_to_mont_fr<<<1, 64, 0, st>>>(dc->consts, 1, ninv_m);
     unsigned glo = (nlo / 64 + 255) / 256, ghi = ((nhi + 63) / 64 + 255) / 256;
     k_pow_table<<<glo, 256, 0, st>>>(dc->lo_g, nlo, cg, 1, nullptr);
     k_pow_table<<<ghi, 256, 0, st>>>(dc->hi_g, nhi, cg, 1ull << COSET_KB, ninv_m);
     k_pow_table<<<glo, 256, 0, st>>>(dc->lo_gi, nlo, cgi, 1, nullptr);
     k_pow_table<<<ghi, 256, 0, st>>>(dc->hi_gi, nhi, cgi, 1ull << COSET_KB, ninv_m);
+    k_pow_table<<<ghi, 256, 0, st>>>(dc->hi_gf, nhi, cg, 1ull << COSET_KB, nullptr);
     ZK_HIP(hipGetLastError());
     ZK_HIP(hipStreamSynchronize(st));
   }

@@ -27,8 +27,6 @@ __constant__ uint32_t W28[8] = {0x725b19f0u, 0x9bd61b6eu, 0x41112ed4u, 0x402d111
                                 0x8ef62abcu, 0x00e0a7ebu, 0xa58a7e85u, 0x2a3c09f0u};
 __constant__ uint32_t W28I[8] = {0x9d18157eu, 0x72394277u, 0xfd399d5du, 0xec9d51f8u,
                                  0x49d5387fu, 0x6117635du, 0x9c229cd5u, 0x01b77519u};
-__constant__ uint32_t GINV[8] = {0xc6666667u, 0xe7f3fbd4u, 0xca4a2d06u, 0xa9ae5ce9u,
-                                 0x33cd568bu, 0x49b9b57cu, 0x5a13d9aau, 0x135b5294u};
 
 __device__ __forceinline__ Fe mont_from_canon(const uint32_t* c) { return to_mont<FrP>(ldc_fe(c)); }
 
@@ -61,77 +59,142 @@ __global__ void __launch_bounds__(256) k_ntt_twiddles(uint32_t* __restrict__ tw,
   }
 }
 
-// One group of `k` stages.  Sub-transform q -> (blk, col): col = q mod 2^(a-k),
-// blk = q / 2^(a-k); element j of it lives at blk*2^a + col + j*2^(a-k).
+// One group of `k` <= 8 stages over a tile of 2048 elements.  Sub-transform
+// q -> (blk, col): col = q mod 2^(a-k), blk = q / 2^(a-k); its element j lives
+// at blk*2^a + col + j*2^(a-k).  Tile index e = j*2^lsub + s (lsub = 11-k,
+// s = sub-transform within the workgroup, q = blockIdx*2^lsub + s), so the 2^lsub
+// adjacent columns of one j form a contiguous 2^lsub*32-B burst in HBM.
 // DIT=false: DIF stages m = 2^a .. 2^(a-k+1); DIT=true: m = 2^(a-k+1) .. 2^a.
+//
+// Radix-8 rounds: every thread holds 8 elements in registers -- the tile
+// indices base | t<<lo, t < 8 -- and runs up to three stages on them (12
+// butterflies, 4 independent multiplies per stage for ILP).  Rounds meet in
+// LDS (limb-major, XOR-swizzled so every wave's 64 lanes hit 64 banks), so a
+// group of 8 stages costs 2 LDS exchanges instead of 8 read/write passes.  The
+// first round loads straight from HBM and the last stores straight back.
 constexpr int NTT_TILE = 2048;
-template <bool DIT>
-__global__ void __launch_bounds__(256) k_ntt_group(uint32_t* __restrict__ data, const uint32_t* __restrict__ tw,
-                                                   uint32_t logn, uint32_t a, uint32_t k) {
-  extern __shared__ __align__(16) uint32_t lds[];  // [j][sub][9]
-  const uint32_t sub_n = NTT_TILE >> k;            // sub-transforms per workgroup
-  const uint32_t len = 1u << k;
-  const uint32_t colbits = a - k;
-  const uint64_t q0 = (uint64_t)blockIdx.x * sub_n;
-  // load: element e = j*sub_n + s
-  for (uint32_t e = threadIdx.x; e < NTT_TILE; e += blockDim.x) {
-    uint32_t j = e / sub_n, s = e % sub_n;
-    uint64_t q = q0 + s;
-    uint64_t col = q & ((1ull << colbits) - 1), blk = q >> colbits;
-    uint64_t idx = (blk << a) + col + ((uint64_t)j << colbits);
-    Fe v = ld_fe(data + idx * 8);
-#pragma unroll
-    for (int l = 0; l < NL; l++) lds[e * NL + l] = v.v[l];
+
+__device__ __forceinline__ uint32_t ntt_slot(uint32_t e) {
+  uint32_t h = (e >> 6) & 7;
+  return e ^ h ^ (h << 3);
+}
+
+struct NttGroup {
+  uint32_t logn, a, lsub, smask, colbits, colmask, q0;
+  __device__ __forceinline__ size_t gidx(uint32_t e) const {
+    uint32_t q = q0 + (e & smask), j = e >> lsub;
+    return ((size_t)(q >> colbits) << a) + (q & colmask) + ((size_t)j << colbits);
   }
-  __syncthreads();
-  const uint32_t nb = NTT_TILE / 2;
-  for (uint32_t st = 0; st < k; st++) {
-    // local half-distance (in j units) for this stage
-    uint32_t hl = DIT ? (1u << st) : (len >> (st + 1));
-    uint32_t logm = colbits + (DIT ? st + 1 : k - st);  // m = 2^logm
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-      uint32_t s = b % sub_n, pj = b / sub_n;  // pair index within sub-transform
-      uint32_t j0 = (pj / hl) * (2 * hl) + (pj % hl);
-      uint32_t e0 = j0 * sub_n + s, e1 = (j0 + hl) * sub_n + s;
-      Fe u, v;
+};
+
+// u - v + 2r in one signed-carry pass, u, v in [0, 2r): a multiplier input
+// in (0, 4r), which the Montgomery product absorbs (4r * r << 169 r^2).
+__device__ __forceinline__ Fe fr_sub_lazy(const Fe& a, const Fe& b) {
+  Fe r;
+  int32_t c = 0;
 #pragma unroll
-      for (int l = 0; l < NL; l++) {
-        u.v[l] = lds[e0 * NL + l];
-        v.v[l] = lds[e1 * NL + l];
-      }
-      // twiddle index: i mod (m/2) scaled by n/m
-      uint64_t q = q0 + s;
-      uint64_t col = q & ((1ull << colbits) - 1), blk = q >> colbits;
-      uint64_t i = (blk << a) + col + ((uint64_t)j0 << colbits);
-      uint64_t jm = i & ((1ull << (logm - 1)) - 1);
-      uint64_t te = jm << (logn - logm);
-      Fe w = ld_fe(tw + te * 8);
-      Fe x, y;
+  for (int i = 0; i < NL; i++) {
+    int32_t t = (int32_t)(a.v[i] + FrP::P2[i]) - (int32_t)b.v[i] + c;
+    r.v[i] = (uint32_t)t & LMASK;
+    c = t >> 29;
+  }
+  return r;
+}
+
+template <bool DIT, int R>
+__device__ __forceinline__ void ntt_r8_stages(Fe (&x)[8], uint32_t base, uint32_t lo, const uint32_t* __restrict__ tw,
+                                              const NttGroup& g) {
+#pragma unroll
+  for (int si = 0; si < R; si++) {
+    const int rb = DIT ? si : R - 1 - si;  // register bit of this stage
+    const uint32_t lhl = lo + rb - g.lsub;  // j-bit of the pair distance
+    const uint32_t sh = g.logn - (g.colbits + lhl + 1);
+    uint4 w[4][2];  // packed twiddles, unpacked at their butterfly
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const int t0 = ((p >> rb) << (rb + 1)) | (p & ((1 << rb) - 1));
+      const uint32_t e0 = base | ((uint32_t)t0 << lo);
+      const uint32_t col = (g.q0 + (e0 & g.smask)) & g.colmask;
+      const uint32_t jj = (e0 >> g.lsub) & ((1u << lhl) - 1);
+      // omega_m^(i mod m/2) = omega_n^((i mod m/2) * n/m)
+      const uint4* tp = reinterpret_cast<const uint4*>(tw + (size_t)((col + (jj << g.colbits)) << sh) * 8);
+      w[p][0] = tp[0];
+      w[p][1] = tp[1];
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const int t0 = ((p >> rb) << (rb + 1)) | (p & ((1 << rb) - 1)), t1 = t0 | (1 << rb);
+      const uint32_t ww[8] = {w[p][0].x, w[p][0].y, w[p][0].z, w[p][0].w,
+                              w[p][1].x, w[p][1].y, w[p][1].z, w[p][1].w};
+      const Fe wp = unpack(ww);
+      Fe u = x[t0], v = x[t1];
       if (DIT) {
-        Fe t = mul<FrP>(v, w);
-        x = add<FrP>(u, t);
-        y = sub<FrP>(u, t);
+        Fe t = mul<FrP>(v, wp);
+        x[t0] = add<FrP>(u, t);
+        x[t1] = sub<FrP>(u, t);
       } else {
-        x = add<FrP>(u, v);
-        y = mul<FrP>(sub<FrP>(u, v), w);
-      }
-#pragma unroll
-      for (int l = 0; l < NL; l++) {
-        lds[e0 * NL + l] = x.v[l];
-        lds[e1 * NL + l] = y.v[l];
+        x[t0] = add<FrP>(u, v);
+        x[t1] = mul<FrP>(fr_sub_lazy(u, v), wp);
       }
     }
-    __syncthreads();
   }
-  for (uint32_t e = threadIdx.x; e < NTT_TILE; e += blockDim.x) {
-    uint32_t j = e / sub_n, s = e % sub_n;
-    uint64_t q = q0 + s;
-    uint64_t col = q & ((1ull << colbits) - 1), blk = q >> colbits;
-    uint64_t idx = (blk << a) + col + ((uint64_t)j << colbits);
-    Fe v;
+}
+
+template <bool DIT>
+__global__ void __launch_bounds__(256, 2) k_ntt_group(uint32_t* __restrict__ data, const uint32_t* __restrict__ tw,
+                                                   uint32_t logn, uint32_t a, uint32_t k) {
+  extern __shared__ __align__(16) uint32_t lds[];  // [limb][slot]
+  NttGroup g;
+  g.logn = logn;
+  g.a = a;
+  g.lsub = 11 - k;
+  g.smask = (1u << g.lsub) - 1;
+  g.colbits = a - k;
+  g.colmask = (1u << g.colbits) - 1;
+  g.q0 = blockIdx.x << g.lsub;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nr = (k + 2) / 3, rem = k - 3 * (nr - 1);
+  Fe x[8];
+  for (uint32_t r = 0; r < nr; r++) {
+    // DIF: stages run high j-bit -> low, the partial round last;
+    // DIT: low -> high, the partial round first.  Either way b0 <= 8.
+    uint32_t R, b0;
+    if (!DIT) {
+      R = r == nr - 1 ? rem : 3;
+      b0 = 11 - 3 * r - R;
+    } else {
+      R = r == 0 ? rem : 3;
+      b0 = g.lsub + (r == 0 ? 0 : rem + 3 * (r - 1));
+    }
+    const uint32_t lo = b0;
+    const uint32_t base = (tid & ((1u << lo) - 1)) | ((tid >> lo) << (lo + 3));
+    if (r == 0) {
 #pragma unroll
-    for (int l = 0; l < NL; l++) v.v[l] = lds[e * NL + l];
-    st_fe(data + idx * 8, v);
+      for (int t = 0; t < 8; t++) x[t] = ld_fe(data + g.gidx(base | ((uint32_t)t << lo)) * 8);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        const uint32_t sl = ntt_slot(base | ((uint32_t)t << lo));
+#pragma unroll
+        for (int l = 0; l < NL; l++) x[t].v[l] = lds[l * NTT_TILE + sl];
+      }
+      __syncthreads();  // every read of this round is done before the next write
+    }
+    if (R == 3) ntt_r8_stages<DIT, 3>(x, base, lo, tw, g);
+    else if (R == 2) ntt_r8_stages<DIT, 2>(x, base, lo, tw, g);
+    else ntt_r8_stages<DIT, 1>(x, base, lo, tw, g);
+    if (r == nr - 1) {
+#pragma unroll
+      for (int t = 0; t < 8; t++) st_fe(data + g.gidx(base | ((uint32_t)t << lo)) * 8, x[t]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        const uint32_t sl = ntt_slot(base | ((uint32_t)t << lo));
+#pragma unroll
+        for (int l = 0; l < NL; l++) lds[l * NTT_TILE + sl] = x[t].v[l];
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -192,7 +255,23 @@ __device__ __forceinline__ uint32_t brev_bits(uint32_t x, uint32_t bits) { retur
 // workgroup for `mid` swaps tile(mid) with tile(rev(mid)) (or permutes its own
 // tile when mid is a palindrome); workgroups with mid > rev(mid) exit.
 // Values are fully reduced to [0, r) on the way out.
-__global__ void __launch_bounds__(256) k_bitrev_tiled(uint32_t* __restrict__ data, uint32_t logn, uint32_t b) {
+// Optional scaling of the output element at natural index i (the inverse
+// transform's n^-1 and coset factors, folded into this memory-bound pass):
+// mode 1: * c; mode 2: * lo[i mod 2^KB] * hi[i >> KB] (Montgomery multipliers).
+struct BitrevScale {
+  int mode;
+  const uint32_t *c, *lo, *hi;
+};
+__device__ __forceinline__ Fe bitrev_scale(Fe v, uint64_t i, const BitrevScale& sc) {
+  if (sc.mode == 1) v = mul<FrP>(v, ld_fe(sc.c));
+  else if (sc.mode == 2) {
+    v = mul<FrP>(v, ld_fe(sc.lo + (i & ((1u << COSET_KB) - 1)) * 8));
+    v = mul<FrP>(v, ld_fe(sc.hi + (i >> COSET_KB) * 8));
+  }
+  return v;
+}
+__global__ void __launch_bounds__(256) k_bitrev_tiled(uint32_t* __restrict__ data, uint32_t logn, uint32_t b,
+                                                      BitrevScale sc) {
   extern __shared__ __align__(16) uint32_t lds[];  // two tiles [hi][lo][8]
   const uint32_t T = 1u << b, midbits = logn - 2 * b;
   const uint32_t mid = blockIdx.x;
@@ -222,45 +301,28 @@ __global__ void __launch_bounds__(256) k_bitrev_tiled(uint32_t* __restrict__ dat
       uint32_t w[8];
 #pragma unroll
       for (int l = 0; l < 8; l++) w[l] = src[l];
-      Fe v = reduce<FrP>(unpack(w));
       uint64_t oidx = ((uint64_t)rlo << (logn - b)) | ((uint64_t)omid << b) | rhi;
+      Fe v = reduce<FrP>(bitrev_scale(unpack(w), oidx, sc));
       st_fe(data + oidx * 8, v);
     }
   }
 }
 __global__ void __launch_bounds__(256) k_bitrev_naive(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                      uint32_t logn) {
+                                                      uint32_t logn, BitrevScale sc) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (1u << logn)) return;
   uint32_t r = logn ? brev_bits(i, logn) : 0;
-  st_fe(out + (size_t)r * 8, reduce<FrP>(ld_fe(in + (size_t)i * 8)));
+  st_fe(out + (size_t)r * 8, reduce<FrP>(bitrev_scale(ld_fe(in + (size_t)i * 8), r, sc)));
 }
 
-// data[i] = reduce(data[i] * c * g^(+-i)) in natural order; g^i by runs of 64.
-// mode bit0: multiply by n^-1; bit1: coset powers; bit2: inverse coset (g^-i)
-__global__ void __launch_bounds__(256) k_ntt_scale(uint32_t* __restrict__ data, uint32_t logn, int mode) {
-  uint64_t n = 1ull << logn;
-  uint64_t i0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * 64;
-  if (i0 >= n) return;
-  Fe c = one<FrP>();
-  if (mode & 1) {
-    // n^-1 = (2^-1)^logn with 2^-1 = (r+1)/2
-    const uint32_t half_c[8] = {0xf8000001u, 0xa1f0fac9u, 0x3cdcb848u, 0x9419f424u,
-                                0x40c0ac2eu, 0xdc2822dbu, 0x7098d014u, 0x18322739u};
-    Fe hinv = to_mont<FrP>(ldc_fe(half_c));
-    for (uint32_t k = 0; k < logn; k++) c = mul<FrP>(c, hinv);
-  }
-  Fe g = one<FrP>(), cur = c;
-  if (mode & 2) {
-    if (mode & 4) g = mont_from_canon(GINV);
-    else g = to_mont<FrP>(Fe{{5, 0, 0, 0, 0, 0, 0, 0, 0}});
-    cur = mul<FrP>(c, fe_pow_u64(g, i0));
-  }
-  for (int k = 0; k < 64 && i0 + k < n; k++) {
-    uint32_t* p = data + (i0 + k) * 8;
-    st_fe(p, reduce<FrP>(mul<FrP>(ld_fe(p), cur)));
-    if (mode & 2) cur = mul<FrP>(cur, g);
-  }
+// data[i] *= g^i in natural order (forward coset), g^i = lo[i mod 2^KB] * hi[i >> KB]
+__global__ void __launch_bounds__(256) k_ntt_coset_scale(uint32_t* __restrict__ data, uint32_t logn,
+                                                         const uint32_t* __restrict__ lo,
+                                                         const uint32_t* __restrict__ hi) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= (1ull << logn)) return;
+  Fe v = mul<FrP>(ld_fe(data + i * 8), ld_fe(lo + (i & ((1u << COSET_KB) - 1)) * 8));
+  st_fe(data + i * 8, mul<FrP>(v, ld_fe(hi + (i >> COSET_KB) * 8)));
 }
 
 // ------------------------------------------------------------- host side
@@ -321,46 +383,50 @@ int ntt_raw(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit) {
   return 0;
 }
 
-// in-place permutation natural <-> bit-reversed (+ full reduction)
-int ntt_bitrev(zkmi_ctx* ctx, uint32_t* d, uint32_t logn) {
+// in-place permutation natural <-> bit-reversed (+ optional scaling, + full reduction)
+static int ntt_bitrev_scaled(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, BitrevScale sc) {
   hipStream_t st = ctx->stream;
   ScopedKernelTimer tm(ctx, "ntt_bitrev");
   if (logn >= 10) {
     uint32_t b = 5;
     unsigned grid = 1u << (logn - 2 * b);
-    k_bitrev_tiled<<<grid, 256, 2 * (1u << (2 * b)) * 32, st>>>(d, logn, b);
+    k_bitrev_tiled<<<grid, 256, 2 * (1u << (2 * b)) * 32, st>>>(d, logn, b, sc);
   } else {
     uint32_t* tmp;
     ZK_TRY(ctx->ws.get("ntt_tmp_small", ((size_t)1 << logn) * 32, (void**)&tmp));
-    k_bitrev_naive<<<((1u << logn) + 255) / 256, 256, 0, st>>>(d, tmp, logn);
+    k_bitrev_naive<<<((1u << logn) + 255) / 256, 256, 0, st>>>(d, tmp, logn, sc);
     ZK_HIP(hipMemcpyAsync(d, tmp, ((size_t)1 << logn) * 32, hipMemcpyDeviceToDevice, st));
   }
   ZK_HIP(hipGetLastError());
   return 0;
 }
-
-int ntt_scale(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int mode) {
-  uint64_t runs = ((1ull << logn) + 63) / 64;
-  ScopedKernelTimer tm(ctx, "ntt_scale");
-  k_ntt_scale<<<(unsigned)((runs + 255) / 256), 256, 0, ctx->stream>>>(d, logn, mode);
-  ZK_HIP(hipGetLastError());
-  return 0;
+int ntt_bitrev(zkmi_ctx* ctx, uint32_t* d, uint32_t logn) {
+  return ntt_bitrev_scaled(ctx, d, logn, BitrevScale{0, nullptr, nullptr, nullptr});
 }
 
-// natural order in and out (arkworks semantics)
+// natural order in and out (arkworks semantics):
+//   forward: [x_i *= g^i] -> DIF (bit-reversed out) -> bit reversal
+//   inverse: DIF with omega^-1 -> bit reversal fused with * n^-1 [g^-i]
 int ntt_device(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inverse, int coset) {
   if (logn > 28) {
     set_error("ntt: log_n %u > 28 (two-adicity of Fr)", logn);
     return ZKMI_EINVAL;
   }
+  DomainCache dc;
+  ZK_TRY(domain_cache(ctx, logn, &dc));
   if (!inverse) {
-    if (coset) ZK_TRY(ntt_scale(ctx, d, logn, 2));
+    if (coset) {
+      ScopedKernelTimer tm(ctx, "ntt_scale");
+      k_ntt_coset_scale<<<(unsigned)(((1ull << logn) + 255) / 256), 256, 0, ctx->stream>>>(d, logn, dc.lo_g,
+                                                                                           dc.hi_gf);
+      ZK_HIP(hipGetLastError());
+    }
     ZK_TRY(ntt_raw(ctx, d, logn, 0, false));
     ZK_TRY(ntt_bitrev(ctx, d, logn));
   } else {
     ZK_TRY(ntt_raw(ctx, d, logn, 1, false));
-    ZK_TRY(ntt_bitrev(ctx, d, logn));
-    ZK_TRY(ntt_scale(ctx, d, logn, coset ? (1 | 2 | 4) : 1));
+    BitrevScale sc = coset ? BitrevScale{2, nullptr, dc.lo_gi, dc.hi_gi} : BitrevScale{1, dc.ninv_m, nullptr, nullptr};
+    ZK_TRY(ntt_bitrev_scaled(ctx, d, logn, sc));
   }
   return 0;
 }

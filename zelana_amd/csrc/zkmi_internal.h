@@ -132,5 +132,14 @@ int scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_out);
 
 // NTT entry (ntt.hip): in-place on device, natural order
 int ntt_device(zkmi_ctx* ctx, uint32_t* d_data, uint32_t log_n, int inverse, int coset);
+// per-log_n NTT domain tables (Montgomery): g^x = lo[x mod 2^KB] * hi[x >> KB]
+constexpr uint32_t COSET_KB = 14;
+struct DomainCache {
+  uint32_t* consts;  // [n^-1 canon | (g^n - 1)^-1 mont | n^-1 mont]
+  uint32_t* ninv_m;  // = consts + 16
+  uint32_t *lo_g, *hi_g, *lo_gi, *hi_gi;  // hi_g / hi_gi carry the factor n^-1
+  uint32_t* hi_gf;                        // g^(h 2^KB) without n^-1
+};
+int domain_cache(zkmi_ctx* ctx, uint32_t logn, DomainCache* dc);
 
 }  // namespace zk
