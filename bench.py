@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--l2-log-n", type=int, default=22, help="Groth16 domain 2^k for the L2 proof measurement")
     ap.add_argument("--l2-steps", type=int, default=3)
     ap.add_argument("--no-zbatch", action="store_true", help="skip the zelana_batch (batch 70) proof measurement")
+    ap.add_argument("--no-big", action="store_true", help="skip the config-5 global 2^26 MSM (sharded over all ranks)")
+    ap.add_argument("--big-log-n", type=int, default=26, help="global MSM size 2^k of the config-5 measurement")
+    ap.add_argument("--big-steps", type=int, default=5)
     return ap.parse_args()
 
 
@@ -64,18 +67,24 @@ def main():
     import torch
 
     dist = None
+    # one process per GPU; ZKMI_DIST_BACKEND=gloo (+ more ranks than GPUs) only
+    # to rehearse the multi-rank path on a 1-GPU box
+    backend = os.environ.get("ZKMI_DIST_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
+    gpu_index = local_rank % ndev
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(gpu_index)
+        dist.init_process_group(backend)
     from zelana_amd.gpu import Context
 
-    ctx = Context(local_rank)
+    ctx = Context(gpu_index)
     n = 1 << args.log_n
     bases = ctx.bases_generate(seed=1000 + rank, n=n)
     scalars = ctx.scalars_generate(seed=20 + rank, n=n)
-    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else None
+    dev = torch.device("cuda", gpu_index) if torch.cuda.is_available() else None
+    _coll_dev = dev if backend == "nccl" else None  # gloo collectives on host tensors
 
     def sync_all():
         ctx.sync()
@@ -89,7 +98,7 @@ def main():
         if dist is not None:
             from zelana_amd.dist import combine_partials
 
-            return combine_partials(part, dev)
+            return combine_partials(part, _coll_dev)
         return part
 
     def run(k):
@@ -115,7 +124,7 @@ def main():
         dt = time.perf_counter() - t0
         ctx.profile(False)
         if dist is not None:
-            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            t = torch.tensor([dt], dtype=torch.float64, device=_coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         return res, dt
@@ -169,6 +178,9 @@ def main():
     value = pairs_total / elapsed / 1e6
 
     extra = {"msm_stage_ms_per_step": breakdown, "fixed_base_table": table, "msm_plain_no_table": plain}
+    if not args.no_big:
+        extra["msm_global_2_%d" % args.big_log_n] = bench_msm_sharded(
+            ctx, args.big_log_n, args.big_steps, world, rank, dist, finish, sync_all, _coll_dev)
     if rank == 0 and world == 1 and not args.no_ntt:
         extra["ntt"] = bench_ntt(ctx, args.ntt_log_n)
     if rank == 0 and world == 1 and not args.no_l2:
@@ -238,6 +250,61 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_msm_sharded(ctx, log_total, steps, world, rank, dist, finish, sync_all, coll_dev):
+    """BASELINE.json configs[4]: ONE global BN254 G1 MSM of 2^log_total
+    point-scalar pairs, point-sharded over the world's ranks (strong scaling:
+    rank r owns elements [r*N/W, (r+1)*N/W) of the same global set, resident
+    with its fixed-base table), partials combined by an RCCL all-gather + exact
+    group-law sum.  The result is independent of the world size, so
+    result_sha256 must agree between the N=1/2/4/8 runs."""
+    import hashlib
+
+    total = 1 << log_total
+    per = total // world
+    t0 = time.perf_counter()
+    bases = ctx.bases_generate(seed=1026, n=per, first=rank * per)
+    scalars = ctx.scalars_generate(seed=26, n=per, first=rank * per)
+    gen_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    info = bases.precompute()
+    table_s = time.perf_counter() - t0
+
+    def run(k):
+        pending = ctx.msm_submit(bases, scalars, per)
+        for _ in range(k - 1):
+            nxt = ctx.msm_submit(bases, scalars, per)
+            finish(pending)
+            pending = nxt
+        return finish(pending)
+
+    run(1)
+    sync_all()
+    t0 = time.perf_counter()
+    res = run(steps)
+    sync_all()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    del bases, scalars
+    return {
+        "workload": f"BN254 G1 MSM 2^{log_total} (BASELINE.json configs[4]): one global MSM point-sharded over "
+                    f"{world} GPU(s), {per} resident points + fixed-base table per GPU; partials combined by all-gather + group-law sum",
+        "value": round(total * steps / dt / 1e6, 2),
+        "unit": "Mpoint-scalar/s",
+        "ms_per_msm": round(dt / steps * 1e3, 3),
+        "steps": steps,
+        "n_gpus": world,
+        "scaling": "strong",
+        "table": {"window": info[1], "copies": info[2], "build_s": round(table_s, 2)},
+        "generate_s": round(gen_s, 2),
+        "result_sha256": hashlib.sha256(np.ascontiguousarray(res).tobytes()).hexdigest()[:16],
+    }
 
 
 def bench_ntt(ctx, log_n, steps=5):

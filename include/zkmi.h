@@ -99,6 +99,11 @@ int zkmi_bases_info(const zkmi_bases* b, uint64_t out[4]);
 int zkmi_bases_generate_g1(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** out);
 int zkmi_bases_generate_g2(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** out);
 int zkmi_scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_scalars);
+/* The same streams from global element `first` on: element i of the range is
+ * element first + i of the unsharded set, so a point-sharded MSM over ranks
+ * [r*n, (r+1)*n) sums to the single-GPU result (multi-GPU bench, config 5). */
+int zkmi_bases_generate_range_g1(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, zkmi_bases** out);
+int zkmi_scalars_generate_range(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, void* d_scalars);
 
 /* sum_{i<n} scalars[i] * bases[offset + i]; n <= len - offset.
  * Host scalars (n x 4 u64). Result: canonical affine. */

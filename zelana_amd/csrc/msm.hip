@@ -1124,10 +1124,11 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t& x) {
 }
 __constant__ uint64_t FR_MOD64[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
                                      0x30644e72e131a029ull};
-__global__ void __launch_bounds__(256) k_gen_scalars(uint64_t seed, size_t n, uint64_t* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_gen_scalars(uint64_t seed, size_t first, size_t n, uint64_t* __restrict__ out) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t st = seed * 0x100000001B3ull ^ (i * 0x9E3779B97F4A7C15ull);
+  const size_t gi = first + i;
+  uint64_t st = seed * 0x100000001B3ull ^ (gi * 0x9E3779B97F4A7C15ull);
   uint64_t v[4];
   for (;;) {
     for (int k = 0; k < 4; k++) v[k] = splitmix64(st);
@@ -1155,11 +1156,12 @@ __device__ Fe fq_inv(const Fe& a) {
   return pow<FqP>(a, e);  // a^(q-2)
 }
 template <class G>
-__global__ void __launch_bounds__(256) k_gen_bases(uint64_t seed, size_t n, uint32_t* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_gen_bases(uint64_t seed, size_t first, size_t n, uint32_t* __restrict__ out) {
   using F = typename G::F;
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t st = (seed + 0x51ED270Bull) * 0x100000001B3ull ^ (i * 0xD1B54A32D192ED03ull);
+  const size_t gi = first + i;  // element i of the range is global element first + i
+  uint64_t st = (seed + 0x51ED270Bull) * 0x100000001B3ull ^ (gi * 0xD1B54A32D192ED03ull);
   uint64_t k[4];
   for (int j = 0; j < 4; j++) k[j] = splitmix64(st);
   k[3] &= 0x1FFFFFFFFFFFFFFFull;  // 253 bits < r
@@ -1267,7 +1269,7 @@ __global__ void __launch_bounds__(256) k_bases_export(const uint32_t* __restrict
   for (int c = 0; c < G::PW / 8; c++) st_fe(q + 8 * c, from_mont<FqP>(ld_fe(p + 8 * c)));
 }
 
-int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t n, zkmi_bases** out) {
+int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t first, size_t n, zkmi_bases** out) {
   int pw = g2 ? 32 : 16;
   uint32_t* d_pts = nullptr;
   if (hipMalloc(&d_pts, std::max<size_t>(1, n) * pw * 4) != hipSuccess) {
@@ -1277,8 +1279,8 @@ int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t n, zkmi_bases** 
   }
   if (n) {
     unsigned grid = (unsigned)((n + 255) / 256);
-    if (g2) k_gen_bases<G2T><<<grid, 256, 0, ctx->stream>>>(seed, n, d_pts);
-    else k_gen_bases<G1T><<<grid, 256, 0, ctx->stream>>>(seed, n, d_pts);
+    if (g2) k_gen_bases<G2T><<<grid, 256, 0, ctx->stream>>>(seed, first, n, d_pts);
+    else k_gen_bases<G1T><<<grid, 256, 0, ctx->stream>>>(seed, first, n, d_pts);
     ZK_HIP(hipGetLastError());
   }
   ZK_HIP(hipStreamSynchronize(ctx->stream));
@@ -1305,9 +1307,9 @@ int bases_export(const zkmi_bases* b, uint64_t* host_out) {
   ZK_HIP(hipStreamSynchronize(ctx->stream));
   return 0;
 }
-int scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_out) {
+int scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, void* d_out) {
   if (n) {
-    k_gen_scalars<<<(unsigned)((n + 255) / 256), 256, 0, ctx->stream>>>(seed, n, (uint64_t*)d_out);
+    k_gen_scalars<<<(unsigned)((n + 255) / 256), 256, 0, ctx->stream>>>(seed, first, n, (uint64_t*)d_out);
     ZK_HIP(hipGetLastError());
   }
   ZK_HIP(hipStreamSynchronize(ctx->stream));

@@ -271,7 +271,13 @@ int zkmi_bases_generate_g2(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** 
   return bases_generate(ctx, 1, seed, n, out);
 }
 int zkmi_scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_scalars) {
-  return scalars_generate(ctx, seed, n, d_scalars);
+  return scalars_generate(ctx, seed, 0, n, d_scalars);
+}
+int zkmi_bases_generate_range_g1(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, zkmi_bases** out) {
+  return bases_generate(ctx, 0, seed, first, n, out);
+}
+int zkmi_scalars_generate_range(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, void* d_scalars) {
+  return scalars_generate(ctx, seed, first, n, d_scalars);
 }
 
 static int msm_host_scalars(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_t* scalars, size_t n,

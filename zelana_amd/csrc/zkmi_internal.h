@@ -124,11 +124,14 @@ int bases_upload(zkmi_ctx* ctx, int g2, const uint64_t* host_affine, size_t n, z
 int bases_from_device_canon(zkmi_ctx* ctx, int g2, const uint32_t* d_canon, size_t n, zkmi_bases** out);
 
 // synthetic inputs generated in HBM (bench) and canonical export (checks)
-int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t n, zkmi_bases** out);
+int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t first, size_t n, zkmi_bases** out);
+inline int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t n, zkmi_bases** out) {
+  return bases_generate(ctx, g2, seed, 0, n, out);
+}
 int bases_export(const zkmi_bases* b, uint64_t* host_out);
 int bases_precompute(zkmi_bases* b, int c, int factor);
 int table_window(size_t N);
-int scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_out);
+int scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, void* d_out);
 
 // NTT entry (ntt.hip): in-place on device, natural order
 int ntt_device(zkmi_ctx* ctx, uint32_t* d_data, uint32_t log_n, int inverse, int coset);

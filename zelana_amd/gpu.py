@@ -46,10 +46,15 @@ class DeviceBuffer:
 
 
 class Bases:
-    def __init__(self, ctx: "Context", points, g2: bool, *, generate_seed=None, n=None):
+    def __init__(self, ctx: "Context", points, g2: bool, *, generate_seed=None, n=None, first=0):
         if generate_seed is not None:
             self.ctx, self.g2, self.n = ctx, g2, n
             self.h = vp()
+            if first:
+                assert not g2, "ranged generation is G1 only"
+                check(lib().zkmi_bases_generate_range_g1(ctx.h, generate_seed, first, n, ctypes.byref(self.h)),
+                      "zkmi_bases_generate_range_g1")
+                return
             f = lib().zkmi_bases_generate_g2 if g2 else lib().zkmi_bases_generate_g1
             check(f(ctx.h, generate_seed, n, ctypes.byref(self.h)), "zkmi_bases_generate")
             return
@@ -129,12 +134,13 @@ class Context:
     def bases_g2(self, points):
         return Bases(self, points, True)
 
-    def bases_generate(self, seed: int, n: int, g2: bool = False):
-        return Bases(self, None, g2, generate_seed=seed, n=n)
+    def bases_generate(self, seed: int, n: int, g2: bool = False, first: int = 0):
+        """Synthetic bases k_i*G generated in HBM; elements [first, first+n) of seed's set."""
+        return Bases(self, None, g2, generate_seed=seed, n=n, first=first)
 
-    def scalars_generate(self, seed: int, n: int) -> DeviceBuffer:
+    def scalars_generate(self, seed: int, n: int, first: int = 0) -> DeviceBuffer:
         buf = DeviceBuffer(self, max(1, n) * 32)
-        check(lib().zkmi_scalars_generate(self.h, seed, n, buf.ptr), "zkmi_scalars_generate")
+        check(lib().zkmi_scalars_generate_range(self.h, seed, first, n, buf.ptr), "zkmi_scalars_generate_range")
         return buf
 
     def msm(self, bases: Bases, scalars, offset: int = 0):
