@@ -1,0 +1,69 @@
+"""GPU parity for the reference's own prove path: Groth16Prover.prove(inputs,
+witness) (prover.rs:350-425) over L2BlockCircuit (l2_block.py), with the
+keygen.rs flow (seed 0 over dummy()) run by the oracle.
+
+The GPU proof must equal the oracle's proof on the same R1CS, z and r, s
+(StdRng::seed_from_u64(batch_id)), for an honest batch and for the
+reference's usual unsatisfied one (blake3 batch hash).
+The R1CS itself is parity-unpinned (see l2block.py).
+"""
+import numpy as np
+import pytest
+
+from test_gpu_groth16 import _oracle_prove, _setup
+
+pytestmark = pytest.mark.gpu
+
+SENDER, RECIPIENT = bytes([1] * 32), bytes([2] * 32)
+
+
+@pytest.fixture(scope="module")
+def prover():
+    from zelana_amd import gpu
+    from zelana_amd.l2block import L2BlockCircuit
+    from zelana_amd.prover import Groth16Prover
+    ctx = gpu.Context(0)
+    cs, _, _ = L2BlockCircuit.dummy().synthesize()
+    opk, pkb, _, (st, keep) = _setup(cs, 0)  # keygen.rs:87-91
+    pk = gpu.ProvingKey(ctx, pkb, True)
+    pk.precompute()
+    p = Groth16Prover(ctx, pk, pk.vk_bytes())
+    yield p, opk
+    import oracle_ctypes as O
+    O.lib().oracle_pk_free(opk)
+    pk.close()
+    ctx.close()
+
+
+def _batch(batch_id, amount, consistent):
+    from zelana_amd.l2block import L2BlockCircuit, TransactionWitness
+    from zelana_amd.prover import AccountStateSnapshot, BatchPublicInputs, BatchWitness, Transfer
+    w = BatchWitness(transactions=[Transfer(SENDER, RECIPIENT, amount)],
+                     pre_account_states=[AccountStateSnapshot(SENDER, 1000), AccountStateSnapshot(RECIPIENT, 0)])
+    inp = BatchPublicInputs(batch_id=batch_id, batch_hash=bytes(range(32)))  # blake3-like: not the circuit's
+    if consistent:
+        c = L2BlockCircuit(batch_id=batch_id, transactions=[TransactionWitness(SENDER, RECIPIENT, amount)],
+                           initial_accounts={SENDER: 1000, RECIPIENT: 0}).with_consistent_inputs()
+        inp = BatchPublicInputs(c.pre_state_root, c.post_state_root, c.pre_shielded_root, c.post_shielded_root,
+                                c.withdrawal_root, c.batch_hash, batch_id)
+    return inp, w
+
+
+@pytest.mark.parametrize("batch_id,amount,consistent", [(0, 100, True), (41, 7, True), (42, 100, False)])
+def test_l2_prove_matches_oracle(prover, batch_id, amount, consistent):
+    import oracle_ctypes as O
+    from zelana_amd.prover import l2_block_circuit
+    from zelana_amd.rng import StdRng
+    p, opk = prover
+    inp, w = _batch(batch_id, amount, consistent)
+    proof = p.prove(inp, w)
+    assert len(proof.proof_bytes) == 256 and p.verify(proof)
+    cs, z = l2_block_circuit(inp, w)
+    assert cs.is_satisfied(z) == consistent
+    rng = StdRng.seed_from_u64(batch_id)
+    r, s = rng.fr_rand(), rng.fr_rand()
+    st, keep = O.make_r1cs(cs)
+    zz = np.array([O.int_to_limbs(v) for v in z], np.uint64)
+    a, b, c = _oracle_prove(opk, st, zz, r, s)
+    assert np.array_equal(proof.a, a) and np.array_equal(proof.b, b) and np.array_equal(proof.c, c)
+    assert proof.proof_bytes == p.proof_to_solana_bytes(a, b, c)

@@ -13,8 +13,10 @@ polynomial operation runs in libzkmi.so on the MI355X:
                                               r, s = Fr::rand x2, zkmi_groth16_prove
   proof_to_solana_bytes       (:304-334)  -> 256 B (-A || B || C, LE coordinates)
   compute_vk_hash             (:289-294)  -> blake3(compressed vk)
-Circuit synthesis (L2BlockCircuit, prover/src/l2_circuit.rs) is pluggable: a
-`circuit` callable maps (inputs, witness) to (R1CS, full assignment z).
+Circuit synthesis defaults to the reference's L2BlockCircuit
+(prover/src/l2_circuit.rs, restated in l2block.py; `l2_block_circuit` below
+follows the witness mapping of prover.rs:357-405).  Any other `circuit`
+callable mapping (inputs, witness) to (R1CS, full assignment z) plugs in.
 """
 from __future__ import annotations
 
@@ -43,6 +45,66 @@ class BatchPublicInputs:
 
 
 @dataclass
+class Transfer:
+    """TransactionType::Transfer fields the prover reads (prover.rs:362-366)."""
+    signer_pubkey: bytes
+    to: bytes
+    amount: int
+
+
+@dataclass
+class Withdraw:
+    """TransactionType::Withdraw fields the prover reads (prover.rs:384-387)."""
+    to_l1_address: bytes
+    amount: int
+
+
+@dataclass
+class AccountStateSnapshot:
+    """prover.rs:93-106 (the prover reads account_id and balance)."""
+    account_id: bytes
+    balance: int
+    nonce: int = 0
+    merkle_proof: list = field(default_factory=list)
+    path_indices: list = field(default_factory=list)
+    position: int = 0
+
+
+@dataclass
+class BatchWitness:
+    """prover.rs:78-90; other TransactionType variants may appear in
+    `transactions` as any other object and are skipped, as the reference does."""
+    transactions: list = field(default_factory=list)
+    results: list = field(default_factory=list)
+    pre_account_states: list = field(default_factory=list)
+    transfer_witnesses: list = field(default_factory=list)
+    withdrawal_witnesses: list = field(default_factory=list)
+
+
+def l2_circuit_of(inputs: "BatchPublicInputs", witness: BatchWitness):
+    """Groth16Prover::prove's circuit construction (prover.rs:357-405)."""
+    from .l2block import L2BlockCircuit, TransactionWitness, WithdrawalWitness
+
+    txs = [TransactionWitness(t.signer_pubkey, t.to, t.amount) for t in witness.transactions if isinstance(t, Transfer)]
+    accounts = {}
+    for st in witness.pre_account_states:
+        accounts[bytes(st.account_id)] = int(st.balance)
+    wds = [WithdrawalWitness(w.to_l1_address, w.amount) for w in witness.transactions if isinstance(w, Withdraw)]
+    return L2BlockCircuit(pre_state_root=inputs.pre_state_root, post_state_root=inputs.post_state_root,
+                          pre_shielded_root=inputs.pre_shielded_root, post_shielded_root=inputs.post_shielded_root,
+                          withdrawal_root=inputs.withdrawal_root, batch_hash=inputs.batch_hash,
+                          batch_id=inputs.batch_id, transactions=txs, initial_accounts=accounts,
+                          shielded_commitments=[],  # prover.rs:402 (TODO in the reference)
+                          withdrawals=wds)
+
+
+def l2_block_circuit(inputs: "BatchPublicInputs", witness: BatchWitness):
+    """Default synthesizer: (R1CS, z) of L2BlockCircuit for this batch."""
+    cs, z, _ = l2_circuit_of(inputs, witness).synthesize()
+    return cs, z
+
+
+@dataclass
 class BatchProof:
     public_inputs: BatchPublicInputs
     proof_bytes: bytes
@@ -61,7 +123,7 @@ class Groth16Prover:
         self.pk = pk
         self.verifying_key = vk_bytes
         self.vk_hash = blake3(vk_bytes)
-        self.circuit = circuit
+        self.circuit = circuit if circuit is not None else l2_block_circuit
 
     @classmethod
     def from_bytes(cls, pk_bytes: bytes, vk_bytes: bytes, device: int = 0, circuit=None, compressed=True,
@@ -88,8 +150,7 @@ class Groth16Prover:
 
     # ---------------------------------------------------------- BatchProver
     def prove(self, inputs: BatchPublicInputs, witness) -> BatchProof:
-        if self.circuit is None:
-            raise NotImplementedError("no circuit synthesizer configured (L2BlockCircuit R1CS is SURVEY §8f next)")
+        """prover.rs:350-425: synthesize, r/s from StdRng(batch_id), prove on the GPU."""
         cs, z = self.circuit(inputs, witness)
         return self.prove_r1cs(cs, z, inputs)
 
