@@ -36,6 +36,8 @@ struct zkmi_pk {
 namespace zk {
 
 int ntt_raw(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit);
+int ntt_raw_epi(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit, int epi, const uint32_t* lo,
+                const uint32_t* hi);
 int ntt_bitrev(zkmi_ctx* ctx, uint32_t* d, uint32_t logn);
 
 // ------------------------------------------------------------ decoding
@@ -274,18 +276,6 @@ __global__ void __launch_bounds__(256) k_pow_table(uint32_t* __restrict__ tab, u
     cur = mul<FrP>(cur, bs);
   }
 }
-// data[p] *= lo[e & (2^kb - 1)] * hi[e >> kb] with e = rev(p)  (coset powers in
-// bit-reversed layout; hi carries the constant factor)
-__global__ void __launch_bounds__(256) k_scale_rev(uint32_t* __restrict__ data, uint32_t logn,
-                                                   const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi,
-                                                   uint32_t kb, int final_reduce) {
-  size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (p >= (1ull << logn)) return;
-  uint32_t e = logn ? (__brev((uint32_t)p) >> (32 - logn)) : 0;
-  Fe v = mul<FrP>(ld_fe(data + p * 8), ld_fe(lo + (size_t)(e & ((1u << kb) - 1)) * 8));
-  v = mul<FrP>(v, ld_fe(hi + (size_t)(e >> kb) * 8));
-  st_fe(data + p * 8, final_reduce ? reduce<FrP>(v) : v);
-}
 // a = (a * b - c) * vinv  (natural order, coset evaluations).  a, b, c are in
 // value form (the data never enter Montgomery form), so the Montgomery product
 // a*b*R^-1 is brought back with one multiplication by R^2.
@@ -468,12 +458,9 @@ static int witness_map_dev(zkmi_ctx* ctx, const DevR1CS& dr, const uint32_t* d_z
   // evaluations -> coefficients (DIF, bit-reversed) -> * n^-1 g^i -> coset
   // evaluations (DIT, natural)
   uint32_t* vecs[3] = {a, b, c};
+  // (the * n^-1 g^i scaling rides on the DIF's innermost pass)
   for (int t = 0; t < 3; t++) {
-    ZK_TRY(ntt_raw(ctx, vecs[t], logn, 1, false));
-    {
-      ScopedKernelTimer tm(ctx, "g16_scale");
-      k_scale_rev<<<gn, 256, 0, st>>>(vecs[t], logn, dc.lo_g, dc.hi_g, COSET_KB, 0);
-    }
+    ZK_TRY(ntt_raw_epi(ctx, vecs[t], logn, 1, false, 2, dc.lo_g, dc.hi_g));
     ZK_TRY(ntt_raw(ctx, vecs[t], logn, 0, true));
   }
   {
@@ -481,11 +468,7 @@ static int witness_map_dev(zkmi_ctx* ctx, const DevR1CS& dr, const uint32_t* d_z
     k_qap_combine<<<gn, 256, 0, st>>>(a, b, c, n, dc.consts + 8);
   }
   // coset evaluations -> coefficients: DIF inverse, * n^-1 g^-i, reduce
-  ZK_TRY(ntt_raw(ctx, a, logn, 1, false));
-  {
-    ScopedKernelTimer tm(ctx, "g16_scale");
-    k_scale_rev<<<gn, 256, 0, st>>>(a, logn, dc.lo_gi, dc.hi_gi, COSET_KB, 1);
-  }
+  ZK_TRY(ntt_raw_epi(ctx, a, logn, 1, false, 2, dc.lo_gi, dc.hi_gi));
   ZK_HIP(hipGetLastError());
   return 0;
 }

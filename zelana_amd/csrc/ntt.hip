@@ -46,7 +46,15 @@ __device__ Fe fe_pow_u64(Fe base, uint64_t e) {
   return r;
 }
 
-// tw[e] = omega^e, e < half.  Each thread: one pow + 63 muls for a run of 64.
+// Twiddle table omega^e, e < half, reduced, stored UNPACKED (9 x 29-bit limbs)
+// in two planes so the butterflies skip the 8 -> 9 limb unpack: limbs 0..7
+// at tw[8e..8e+8) (two 16-B loads), limb 8 at tw[8 half + e].
+__device__ __forceinline__ Fe ld_tw(const uint32_t* __restrict__ tw, uint64_t half, uint64_t e) {
+  const uint4* p = reinterpret_cast<const uint4*>(tw + e * 8);
+  const uint4 a = p[0], b = p[1];
+  return Fe{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, tw[8 * half + e]}};
+}
+// Each thread: one pow + 63 muls for a run of 64.
 __global__ void __launch_bounds__(256) k_ntt_twiddles(uint32_t* __restrict__ tw, uint32_t logn, int inv, uint64_t half) {
   uint64_t run = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   uint64_t e0 = run * 64;
@@ -54,7 +62,10 @@ __global__ void __launch_bounds__(256) k_ntt_twiddles(uint32_t* __restrict__ tw,
   Fe w = root_of_unity(logn, inv != 0);
   Fe cur = fe_pow_u64(w, e0);
   for (int k = 0; k < 64 && e0 + k < half; k++) {
-    st_fe(tw + (e0 + k) * 8, reduce<FrP>(cur));
+    const Fe v = reduce<FrP>(cur);
+#pragma unroll
+    for (int l = 0; l < 8; l++) tw[(e0 + k) * 8 + l] = v.v[l];
+    tw[8 * half + e0 + k] = v.v[8];
     cur = mul<FrP>(cur, w);
   }
 }
@@ -80,9 +91,13 @@ __device__ __forceinline__ uint32_t ntt_slot(uint32_t e) {
 }
 
 struct NttGroup {
-  uint32_t logn, a, lsub, smask, colbits, colmask, q0;
+  uint32_t logn, a, lsub, smask, colbits, colmask, q0, qsh;
+  // sub-transform s of this workgroup is q = q0 + (s << qsh): qsh = 0 packs
+  // adjacent columns (coalesced reads); the permuting last pass takes
+  // sub-transforms 2^qsh blocks apart so that its natural-order writes land
+  // on 2^lsub adjacent elements
   __device__ __forceinline__ size_t gidx(uint32_t e) const {
-    uint32_t q = q0 + (e & smask), j = e >> lsub;
+    uint32_t q = q0 + ((e & smask) << qsh), j = e >> lsub;
     return ((size_t)(q >> colbits) << a) + (q & colmask) + ((size_t)j << colbits);
   }
 };
@@ -101,33 +116,41 @@ __device__ __forceinline__ Fe fr_sub_lazy(const Fe& a, const Fe& b) {
   return r;
 }
 
-template <bool DIT, int R>
-__device__ __forceinline__ void ntt_r8_stages(Fe (&x)[8], uint32_t base, uint32_t lo, const uint32_t* __restrict__ tw,
+// TRIV: the round touches stages whose twiddles are omega^0 for every pair p
+// with p mod 2^rb == 0 (the register round at tile bit lsub of a group with
+// no column bits: the last DIF / first DIT round of the innermost group);
+// those multiplications by one are skipped (value form: x * R * R^-1 = x).
+template <bool DIT, int R, bool TRIV, int EPT>
+__device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint32_t lo, const uint32_t* __restrict__ tw,
                                               const NttGroup& g) {
+  constexpr int NP = EPT / 2;  // butterflies per stage per thread
 #pragma unroll
   for (int si = 0; si < R; si++) {
     const int rb = DIT ? si : R - 1 - si;  // register bit of this stage
     const uint32_t lhl = lo + rb - g.lsub;  // j-bit of the pair distance
     const uint32_t sh = g.logn - (g.colbits + lhl + 1);
-    uint4 w[4][2];  // packed twiddles, unpacked at their butterfly
+    const uint64_t half = 1ull << (g.logn - 1);
+    Fe w[NP];  // twiddles (unpacked planes)
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
+    for (int p = 0; p < NP; p++) {
+      if (TRIV && (p & ((1 << rb) - 1)) == 0) continue;
       const int t0 = ((p >> rb) << (rb + 1)) | (p & ((1 << rb) - 1));
       const uint32_t e0 = base | ((uint32_t)t0 << lo);
-      const uint32_t col = (g.q0 + (e0 & g.smask)) & g.colmask;
+      const uint32_t col = (g.q0 + ((e0 & g.smask) << g.qsh)) & g.colmask;
       const uint32_t jj = (e0 >> g.lsub) & ((1u << lhl) - 1);
       // omega_m^(i mod m/2) = omega_n^((i mod m/2) * n/m)
-      const uint4* tp = reinterpret_cast<const uint4*>(tw + (size_t)((col + (jj << g.colbits)) << sh) * 8);
-      w[p][0] = tp[0];
-      w[p][1] = tp[1];
+      w[p] = ld_tw(tw, half, (uint64_t)((col + (jj << g.colbits)) << sh));
     }
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
+    for (int p = 0; p < NP; p++) {
       const int t0 = ((p >> rb) << (rb + 1)) | (p & ((1 << rb) - 1)), t1 = t0 | (1 << rb);
-      const uint32_t ww[8] = {w[p][0].x, w[p][0].y, w[p][0].z, w[p][0].w,
-                              w[p][1].x, w[p][1].y, w[p][1].z, w[p][1].w};
-      const Fe wp = unpack(ww);
       Fe u = x[t0], v = x[t1];
+      if (TRIV && (p & ((1 << rb) - 1)) == 0) {
+        x[t0] = add<FrP>(u, v);
+        x[t1] = sub<FrP>(u, v);
+        continue;
+      }
+      const Fe wp = w[p];
       if (DIT) {
         Fe t = mul<FrP>(v, wp);
         x[t0] = add<FrP>(u, t);
@@ -140,58 +163,113 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[8], uint32_t base, uint32_
   }
 }
 
-template <bool DIT>
-__global__ void __launch_bounds__(256, 2) k_ntt_group(uint32_t* __restrict__ data, const uint32_t* __restrict__ tw,
-                                                   uint32_t logn, uint32_t a, uint32_t k) {
+// Element-wise work folded into the first / last pass of a transform (these
+// would otherwise be separate HBM-bound passes over the vector):
+//   PRO 1: x_i *= g^i = lo[i mod 2^KB] * hi[i >> KB] at natural index i, on
+//          the first loads (forward coset; DIF first group reads natural order)
+//   EPI 1: x *= c;  EPI 2: x *= lo[i mod 2^KB] * hi[i >> KB], with i the
+//          natural index of the element (bit reversal of its DIF position)
+//   PERM:  the innermost DIF group writes natural order, out of place, so
+//          natural -> natural needs no bit-reversal pass
+// Outputs of EPI / PERM passes are fully reduced (canonical).
+struct NttIo {
+  const uint32_t *lo, *hi, *c;
+};
+__device__ __forceinline__ Fe ntt_tab_scale(Fe v, uint64_t i, const NttIo& io) {
+  v = mul<FrP>(v, ld_fe(io.lo + (i & ((1u << COSET_KB) - 1)) * 8));
+  return mul<FrP>(v, ld_fe(io.hi + (i >> COSET_KB) * 8));
+}
+
+// TB = log2(tile), RB = log2(elements per thread): (11, 3) = 2048-element
+// tiles in radix-8 register rounds (72 KB LDS, 2 waves/SIMD); (10, 2) =
+// 1024-element tiles in radix-4 rounds (36 KB LDS, <= 128 VGPRs: 4 waves/SIMD
+// to hide the load and twiddle latency the 2-wave form exposes).
+
+template <bool DIT, int PRO, int EPI, bool PERM, int TB, int RB>
+__global__ void __launch_bounds__(256, (RB == 3 ? 2 : 4)) k_ntt_group(const uint32_t* src, uint32_t* dst,
+                                                                          const uint32_t* __restrict__ tw, uint32_t logn,
+                                                                          uint32_t a, uint32_t k, NttIo io) {
+  constexpr int TILE = 1 << TB, EPT = 1 << RB;
   extern __shared__ __align__(16) uint32_t lds[];  // [limb][slot]
   NttGroup g;
   g.logn = logn;
   g.a = a;
-  g.lsub = 11 - k;
+  g.lsub = TB - k;
   g.smask = (1u << g.lsub) - 1;
   g.colbits = a - k;
   g.colmask = (1u << g.colbits) - 1;
-  g.q0 = blockIdx.x << g.lsub;
+  if (PERM) {  // innermost group: colbits == 0, one block per sub-transform
+    g.q0 = blockIdx.x;
+    g.qsh = logn - k - g.lsub;
+  } else {
+    g.q0 = blockIdx.x << g.lsub;
+    g.qsh = 0;
+  }
   const uint32_t tid = threadIdx.x;
-  const uint32_t nr = (k + 2) / 3, rem = k - 3 * (nr - 1);
-  Fe x[8];
+  const uint32_t nr = (k + RB - 1) / RB, rem = k - RB * (nr - 1);
+  const bool triv_group = g.colbits == 0;
+  Fe x[EPT];
   for (uint32_t r = 0; r < nr; r++) {
     // DIF: stages run high j-bit -> low, the partial round last;
-    // DIT: low -> high, the partial round first.  Either way b0 <= 8.
+    // DIT: low -> high, the partial round first.
     uint32_t R, b0;
     if (!DIT) {
-      R = r == nr - 1 ? rem : 3;
-      b0 = 11 - 3 * r - R;
+      R = r == nr - 1 ? rem : RB;
+      b0 = TB - RB * r - R;
     } else {
-      R = r == 0 ? rem : 3;
-      b0 = g.lsub + (r == 0 ? 0 : rem + 3 * (r - 1));
+      R = r == 0 ? rem : RB;
+      b0 = g.lsub + (r == 0 ? 0 : rem + RB * (r - 1));
     }
     const uint32_t lo = b0;
-    const uint32_t base = (tid & ((1u << lo) - 1)) | ((tid >> lo) << (lo + 3));
+    const uint32_t base = (tid & ((1u << lo) - 1)) | ((tid >> lo) << (lo + RB));
     if (r == 0) {
 #pragma unroll
-      for (int t = 0; t < 8; t++) x[t] = ld_fe(data + g.gidx(base | ((uint32_t)t << lo)) * 8);
+      for (int t = 0; t < EPT; t++) {
+        const size_t gi = g.gidx(base | ((uint32_t)t << lo));
+        x[t] = ld_fe(src + gi * 8);
+        if (PRO == 1) x[t] = ntt_tab_scale(x[t], gi, io);
+      }
     } else {
 #pragma unroll
-      for (int t = 0; t < 8; t++) {
+      for (int t = 0; t < EPT; t++) {
         const uint32_t sl = ntt_slot(base | ((uint32_t)t << lo));
 #pragma unroll
-        for (int l = 0; l < NL; l++) x[t].v[l] = lds[l * NTT_TILE + sl];
+        for (int l = 0; l < NL; l++) x[t].v[l] = lds[l * TILE + sl];
       }
       __syncthreads();  // every read of this round is done before the next write
     }
-    if (R == 3) ntt_r8_stages<DIT, 3>(x, base, lo, tw, g);
-    else if (R == 2) ntt_r8_stages<DIT, 2>(x, base, lo, tw, g);
-    else ntt_r8_stages<DIT, 1>(x, base, lo, tw, g);
+    // the round at tile bit lsub of the innermost group has omega^0 pairs
+    const bool triv = triv_group && lo == g.lsub;
+    if (R == 3) {
+      if (triv) ntt_r8_stages<DIT, 3, true, EPT>(x, base, lo, tw, g);
+      else ntt_r8_stages<DIT, 3, false, EPT>(x, base, lo, tw, g);
+    } else if (R == 2) {
+      if (triv) ntt_r8_stages<DIT, 2, true, EPT>(x, base, lo, tw, g);
+      else ntt_r8_stages<DIT, 2, false, EPT>(x, base, lo, tw, g);
+    } else {
+      if (triv) ntt_r8_stages<DIT, 1, true, EPT>(x, base, lo, tw, g);
+      else ntt_r8_stages<DIT, 1, false, EPT>(x, base, lo, tw, g);
+    }
     if (r == nr - 1) {
 #pragma unroll
-      for (int t = 0; t < 8; t++) st_fe(data + g.gidx(base | ((uint32_t)t << lo)) * 8, x[t]);
+      for (int t = 0; t < EPT; t++) {
+        const size_t gi = g.gidx(base | ((uint32_t)t << lo));
+        if (EPI == 0 && !PERM) {
+          st_fe(dst + gi * 8, x[t]);
+        } else {
+          const uint64_t ni = __brev((uint32_t)gi) >> (32 - logn);  // natural index (DIF output)
+          Fe v = x[t];
+          if (EPI == 1) v = mul<FrP>(v, ld_fe(io.c));
+          if (EPI == 2) v = ntt_tab_scale(v, ni, io);
+          st_fe(dst + (PERM ? ni : gi) * 8, reduce<FrP>(v));
+        }
+      }
     } else {
 #pragma unroll
-      for (int t = 0; t < 8; t++) {
+      for (int t = 0; t < EPT; t++) {
         const uint32_t sl = ntt_slot(base | ((uint32_t)t << lo));
 #pragma unroll
-        for (int l = 0; l < NL; l++) lds[l * NTT_TILE + sl] = x[t].v[l];
+        for (int l = 0; l < NL; l++) lds[l * TILE + sl] = x[t].v[l];
       }
       __syncthreads();
     }
@@ -222,7 +300,7 @@ __global__ void __launch_bounds__(256) k_ntt_small(uint32_t* __restrict__ data, 
         v.v[l] = lds[i1 * NL + l];
       }
       uint32_t te = (i0 & (h - 1)) << (logn - logm);
-      Fe w = ld_fe(tw + (size_t)te * 8);
+      Fe w = ld_tw(tw, (uint64_t)n / 2, te);
       Fe x, y;
       if (DIT) {
         Fe t = mul<FrP>(v, w);
@@ -325,6 +403,17 @@ __global__ void __launch_bounds__(256) k_ntt_coset_scale(uint32_t* __restrict__ 
   st_fe(data + i * 8, mul<FrP>(v, ld_fe(hi + (i >> COSET_KB) * 8)));
 }
 
+// x[p] *= lo[i] * hi[i] at natural index i = rev(p), canonical out (small n)
+__global__ void __launch_bounds__(256) k_scale_rev_small(uint32_t* __restrict__ data, uint32_t logn,
+                                                         const uint32_t* __restrict__ lo,
+                                                         const uint32_t* __restrict__ hi) {
+  size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (p >= (1ull << logn)) return;
+  uint32_t e = logn ? (__brev((uint32_t)p) >> (32 - logn)) : 0;
+  Fe v = mul<FrP>(ld_fe(data + p * 8), ld_fe(lo + (size_t)(e & ((1u << COSET_KB) - 1)) * 8));
+  st_fe(data + p * 8, reduce<FrP>(mul<FrP>(v, ld_fe(hi + (size_t)(e >> COSET_KB) * 8))));
+}
+
 // ------------------------------------------------------------- host side
 static int get_twiddles(zkmi_ctx* ctx, uint32_t logn, int inv, const uint32_t** out) {
   char name[64];
@@ -332,7 +421,7 @@ static int get_twiddles(zkmi_ctx* ctx, uint32_t logn, int inv, const uint32_t** 
   bool fresh = ctx->ws.bufs.find(name) == ctx->ws.bufs.end();
   uint64_t half = std::max<uint64_t>(1, (1ull << logn) / 2);
   uint32_t* tw;
-  ZK_TRY(ctx->ws.get(name, half * 32, (void**)&tw));
+  ZK_TRY(ctx->ws.get(name, half * 36, (void**)&tw));
   if (fresh) {
     uint64_t runs = (half + 63) / 64;
     k_ntt_twiddles<<<(unsigned)((runs + 255) / 256), 256, 0, ctx->stream>>>(tw, logn, inv, half);
@@ -342,9 +431,43 @@ static int get_twiddles(zkmi_ctx* ctx, uint32_t logn, int inv, const uint32_t** 
   return 0;
 }
 
+// Group plan of a 2^logn transform: ceil(logn / 8) groups of <= 8 stages
+// (tile = 2048 elements: 8 sub-transforms of 256, or fewer larger ones).
+static std::vector<uint32_t> ntt_groups(uint32_t logn) {
+  int ng = (logn + 7) / 8;  // <= 8 stages per group for either tile shape
+  std::vector<uint32_t> ks(ng, logn / ng);
+  for (uint32_t r = 0; r < logn % ng; r++) ks[r]++;
+  return ks;
+}
+
+// group kernel shape: 1024-element radix-4 tiles (4 waves/SIMD; measured
+// 7% faster than the 2048-element radix-8 form); ZKMI_NTT_TB=11 selects the latter
+static int ntt_tb() {
+  static const int tb = [] {
+    const char* e = getenv("ZKMI_NTT_TB");
+    return e && atoi(e) == 11 ? 11 : 10;
+  }();
+  return tb;
+}
+template <bool DIT, int PRO, int EPI, bool PERM>
+static void launch_group(hipStream_t st, const uint32_t* src, uint32_t* dst, const uint32_t* tw, uint32_t logn,
+                         uint32_t a, uint32_t k, const NttIo& io) {
+  if (ntt_tb() == 10) {
+    const size_t sm = (size_t)1024 * NL * 4;
+    const unsigned grid = (unsigned)((1ull << logn) / 1024);
+    k_ntt_group<DIT, PRO, EPI, PERM, 10, 2><<<grid, 256, sm, st>>>(src, dst, tw, logn, a, k, io);
+  } else {
+    const size_t sm = (size_t)NTT_TILE * NL * 4;
+    const unsigned grid = (unsigned)((1ull << logn) / NTT_TILE);
+    k_ntt_group<DIT, PRO, EPI, PERM, 11, 3><<<grid, 256, sm, st>>>(src, dst, tw, logn, a, k, io);
+  }
+}
+
 // in-place transform in the requested order without scaling:
 // dit=false: natural in -> bit-reversed out; dit=true: bit-reversed in -> natural out
-int ntt_raw(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit) {
+// epi (DIF only): 0 none, 2 = x * lo[i] * hi[i] at natural index i, canonical out
+int ntt_raw_epi(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit, int epi, const uint32_t* lo,
+                const uint32_t* hi) {
   const uint32_t* tw;
   ZK_TRY(get_twiddles(ctx, logn, inv, &tw));
   hipStream_t st = ctx->stream;
@@ -355,20 +478,22 @@ int ntt_raw(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit) {
     if (dit) k_ntt_small<true><<<1, 256, sm, st>>>(d, tw, logn);
     else k_ntt_small<false><<<1, 256, sm, st>>>(d, tw, logn);
     ZK_HIP(hipGetLastError());
+    if (epi) {
+      ScopedKernelTimer tm2(ctx, "ntt_scale");
+      k_scale_rev_small<<<(unsigned)(((1ull << logn) + 255) / 256), 256, 0, st>>>(d, logn, lo, hi);
+      ZK_HIP(hipGetLastError());
+    }
     return 0;
   }
-  // groups of <= 8 stages (tile = 2048 elements: 8 sub-transforms of 256 or
-  // fewer larger ones when k > 8); balance group sizes
-  int ng = (logn + 7) / 8;
-  std::vector<uint32_t> ks(ng, logn / ng);
-  for (uint32_t r = 0; r < logn % ng; r++) ks[r]++;
-  size_t sm = (size_t)NTT_TILE * NL * 4;
-  unsigned grid = (unsigned)((1ull << logn) / NTT_TILE);
+  const std::vector<uint32_t> ks = ntt_groups(logn);
+  const int ng = (int)ks.size();
+  const NttIo io{lo, hi, nullptr};
   if (!dit) {
     uint32_t a = logn;
     for (int g = 0; g < ng; g++) {
       ScopedKernelTimer tm(ctx, "ntt_group");
-      k_ntt_group<false><<<grid, 256, sm, st>>>(d, tw, logn, a, ks[g]);
+      if (g == ng - 1 && epi == 2) launch_group<false, 0, 2, false>(st, d, d, tw, logn, a, ks[g], io);
+      else launch_group<false, 0, 0, false>(st, d, d, tw, logn, a, ks[g], io);
       a -= ks[g];
     }
   } else {
@@ -376,11 +501,14 @@ int ntt_raw(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit) {
     for (int g = ng - 1; g >= 0; g--) {
       a += ks[g];
       ScopedKernelTimer tm(ctx, "ntt_group");
-      k_ntt_group<true><<<grid, 256, sm, st>>>(d, tw, logn, a, ks[g]);
+      launch_group<true, 0, 0, false>(st, d, d, tw, logn, a, ks[g], io);
     }
   }
   ZK_HIP(hipGetLastError());
   return 0;
+}
+int ntt_raw(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit) {
+  return ntt_raw_epi(ctx, d, logn, inv, dit, 0, nullptr, nullptr);
 }
 
 // in-place permutation natural <-> bit-reversed (+ optional scaling, + full reduction)
@@ -404,9 +532,14 @@ int ntt_bitrev(zkmi_ctx* ctx, uint32_t* d, uint32_t logn) {
   return ntt_bitrev_scaled(ctx, d, logn, BitrevScale{0, nullptr, nullptr, nullptr});
 }
 
-// natural order in and out (arkworks semantics):
-//   forward: [x_i *= g^i] -> DIF (bit-reversed out) -> bit reversal
-//   inverse: DIF with omega^-1 -> bit reversal fused with * n^-1 [g^-i]
+// natural order in and out (arkworks semantics), DIF passes only:
+//   forward: first pass reads d (x_i *= g^i folded in for the coset),
+//            middle passes in place in a scratch vector, the innermost
+//            group writes natural order back into d (PERM)
+//   inverse: the same with omega^-1 and * n^-1 [g^-i] folded into the
+//            permuting pass
+// Small transforms (one tile or less) keep the single-workgroup kernel and
+// a separate bit reversal.
 int ntt_device(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inverse, int coset) {
   if (logn > 28) {
     set_error("ntt: log_n %u > 28 (two-adicity of Fr)", logn);
@@ -414,20 +547,48 @@ int ntt_device(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inverse, int coset
   }
   DomainCache dc;
   ZK_TRY(domain_cache(ctx, logn, &dc));
-  if (!inverse) {
-    if (coset) {
-      ScopedKernelTimer tm(ctx, "ntt_scale");
-      k_ntt_coset_scale<<<(unsigned)(((1ull << logn) + 255) / 256), 256, 0, ctx->stream>>>(d, logn, dc.lo_g,
-                                                                                           dc.hi_gf);
-      ZK_HIP(hipGetLastError());
+  if (logn < 11) {
+    if (!inverse) {
+      if (coset) {
+        ScopedKernelTimer tm(ctx, "ntt_scale");
+        k_ntt_coset_scale<<<(unsigned)(((1ull << logn) + 255) / 256), 256, 0, ctx->stream>>>(d, logn, dc.lo_g,
+                                                                                             dc.hi_gf);
+        ZK_HIP(hipGetLastError());
+      }
+      ZK_TRY(ntt_raw(ctx, d, logn, 0, false));
+      return ntt_bitrev(ctx, d, logn);
     }
-    ZK_TRY(ntt_raw(ctx, d, logn, 0, false));
-    ZK_TRY(ntt_bitrev(ctx, d, logn));
-  } else {
     ZK_TRY(ntt_raw(ctx, d, logn, 1, false));
     BitrevScale sc = coset ? BitrevScale{2, nullptr, dc.lo_gi, dc.hi_gi} : BitrevScale{1, dc.ninv_m, nullptr, nullptr};
-    ZK_TRY(ntt_bitrev_scaled(ctx, d, logn, sc));
+    return ntt_bitrev_scaled(ctx, d, logn, sc);
   }
+  const uint32_t* tw;
+  ZK_TRY(get_twiddles(ctx, logn, inverse, &tw));
+  uint32_t* s;
+  ZK_TRY(ctx->ws.get("ntt_scratch", ((size_t)1 << logn) * 32, (void**)&s));
+  hipStream_t st = ctx->stream;
+  const std::vector<uint32_t> ks = ntt_groups(logn);
+  const int ng = (int)ks.size();
+  const NttIo pro{dc.lo_g, dc.hi_gf, nullptr};
+  NttIo epi{nullptr, nullptr, nullptr};
+  if (inverse) epi = coset ? NttIo{dc.lo_gi, dc.hi_gi, nullptr} : NttIo{nullptr, nullptr, dc.ninv_m};
+  uint32_t a = logn;
+  for (int g = 0; g < ng; g++) {
+    ScopedKernelTimer tm(ctx, "ntt_group");
+    const uint32_t* src = g == 0 ? d : s;
+    if (g < ng - 1) {
+      if (g == 0 && coset && !inverse) launch_group<false, 1, 0, false>(st, src, s, tw, logn, a, ks[g], pro);
+      else launch_group<false, 0, 0, false>(st, src, s, tw, logn, a, ks[g], pro);
+    } else if (!inverse) {
+      launch_group<false, 0, 0, true>(st, src, d, tw, logn, a, ks[g], epi);
+    } else if (coset) {
+      launch_group<false, 0, 2, true>(st, src, d, tw, logn, a, ks[g], epi);
+    } else {
+      launch_group<false, 0, 1, true>(st, src, d, tw, logn, a, ks[g], epi);
+    }
+    a -= ks[g];
+  }
+  ZK_HIP(hipGetLastError());
   return 0;
 }
 
