@@ -685,24 +685,26 @@ int groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, 
   size_t n = pk->n;
   uint32_t* dh;
   ZK_TRY(ctx->ws.get("g16_h", n * 32, (void**)&dh));
-  ZK_TRY(witness_map_dev(ctx, dr, dz, logn, dh));
-  // 5 MSMs back to back; each host epilogue overlaps the next one's kernels
+  // The MSMs over z (l, and a / b_g1 / b_g2, which share the scalars z[1..V]
+  // and so one digits + sort pass) do not need h: they are queued on the MSM
+  // lanes first, the witness map then runs on the context stream beside them
+  // (filling their latency-bound sort / bucket-reduction phases), and the h
+  // MSM follows it.  Each host epilogue overlaps later kernels.
   zkmi_msm_job* jobs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   uint64_t h_acc[8], l_acc[8], a_acc[8], b1_acc[8], b2_acc[16];
   int rc = 0;
-  // h and l on their own lanes; a, b_g1 and b_g2 share the scalars z[1..V]
-  // and so one digits + sort pass (msm_submit_shared)
-  rc = msm_submit(ctx, pk->h_query_rev, 0, dh, n - 1, &jobs[0]);
-  if (!rc) rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
+  rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
   if (!rc) {
     const zkmi_bases* abq[3] = {pk->a_query, pk->b_g1_query, pk->b_g2_query};
     rc = msm_submit_shared(ctx, abq, 3, 1, dz + 8, nv - 1, &jobs[2]);
   }
-  if (!rc) rc = msm_wait(jobs[0], h_acc), jobs[0] = nullptr;
+  if (!rc) rc = witness_map_dev(ctx, dr, dz, logn, dh);
+  if (!rc) rc = msm_submit(ctx, pk->h_query_rev, 0, dh, n - 1, &jobs[0]);
   if (!rc) rc = msm_wait(jobs[1], l_acc), jobs[1] = nullptr;
   if (!rc) rc = msm_wait(jobs[2], a_acc), jobs[2] = nullptr;
   if (!rc) rc = msm_wait(jobs[3], b1_acc), jobs[3] = nullptr;
   if (!rc) rc = msm_wait(jobs[4], b2_acc), jobs[4] = nullptr;
+  if (!rc) rc = msm_wait(jobs[0], h_acc), jobs[0] = nullptr;
   for (auto* j : jobs)
     if (j) msm_job_free(j);
   if (rc) return rc;
