@@ -52,7 +52,7 @@ def _batch(batch_id, amount, consistent):
 @pytest.mark.parametrize("batch_id,amount,consistent", [(0, 100, True), (41, 7, True), (42, 100, False)])
 def test_l2_prove_matches_oracle(prover, batch_id, amount, consistent):
     import oracle_ctypes as O
-    from zelana_amd.prover import l2_block_circuit
+    from zelana_amd.prover import l2_block_circuit, l2_circuit_of
     from zelana_amd.rng import StdRng
     p, opk = prover
     inp, w = _batch(batch_id, amount, consistent)
@@ -67,3 +67,8 @@ def test_l2_prove_matches_oracle(prover, batch_id, amount, consistent):
     a, b, c = _oracle_prove(opk, st, zz, r, s)
     assert np.array_equal(proof.a, a) and np.array_equal(proof.b, b) and np.array_equal(proof.c, c)
     assert proof.proof_bytes == p.proof_to_solana_bytes(a, b, c)
+    # and it is a valid Groth16 proof exactly when the batch is consistent
+    import pairing as PR
+    from zelana_amd.l2block import public_inputs_fr
+    c_ = l2_circuit_of(inp, w)
+    assert PR.verify_with_oracle_vk(opk, 8, public_inputs_fr(c_), proof.a, proof.b, proof.c) == consistent

@@ -55,6 +55,12 @@ def test_zbatch_reduced_proof_matches_oracle(ctx, depth, ntx):
     pk.precompute()
     for g, w in zip(gpu.groth16_prove(ctx, pk, cs, z, r, s), want):
         assert np.array_equal(g, w)
+    # the proof verifies (pairing check) against the setup's verifying key
+    import pairing as PR
+    pub = [O.limbs_to_int(z[i]) for i in range(1, cs.num_instance)]
+    assert PR.verify_with_oracle_vk(opk, cs.num_instance, pub, *got)
+    pub[0] = (pub[0] + 1) % O.R
+    assert not PR.verify_with_oracle_vk(opk, cs.num_instance, pub, *got)
     O.lib().oracle_pk_free(opk)
 
 

@@ -94,14 +94,29 @@ def test_prover_witness_mapping():
     assert c.shielded_commitments == [] and c.batch_id == 9
 
 
-def test_oracle_keygen_and_prove_dummy_shape():
-    """keygen.rs:81-91 (seed 0 over dummy()) then an oracle proof of a batch of
-    that shape; the GPU parity test compares libzkmi against exactly this."""
+def test_oracle_keygen_prove_verify_dummy_shape():
+    """keygen.rs:81-91 (seed 0 over dummy()) then an oracle proof of an honest
+    batch of that shape: the pairing check accepts it for its own public
+    inputs and rejects a changed root (the GPU parity tests compare libzkmi
+    against exactly these oracle proofs)."""
+    import pairing as PR
+    from zelana_amd.l2block import public_inputs_fr
     cs, _, _ = L2BlockCircuit.dummy().synthesize()
     st, keep = O.make_r1cs(cs)
     rng = O.Rng(0)
     opk = O.lib().oracle_groth16_setup(ctypes.byref(st), rng.h, 8)
-    assert opk
-    size = O.lib().oracle_pk_serialize(opk, 1, None, 0)
-    assert size > 0
+    assert opk and O.lib().oracle_pk_serialize(opk, 1, None, 0) > 0
+    c = L2BlockCircuit(batch_id=3, transactions=[TransactionWitness(bytes([1] * 32), bytes([2] * 32), 40)],
+                       initial_accounts={bytes([1] * 32): 50, bytes([2] * 32): 1}).with_consistent_inputs()
+    cs2, z, _ = c.synthesize()
+    st2, keep2 = O.make_r1cs(cs2)
+    zz = np.array([O.int_to_limbs(v) for v in z], np.uint64)
+    a, b, cc = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+    rs = np.concatenate([O.int_to_limbs(11), O.int_to_limbs(22)])
+    assert O.lib().oracle_groth16_prove(opk, ctypes.byref(st2), O.P(zz), None, O.P(rs), 8, O.P(a), O.P(b), O.P(cc),
+                                        None) == 0
+    pub = public_inputs_fr(c)
+    assert PR.verify_with_oracle_vk(opk, 8, pub, a, b, cc)
+    pub[1] = (pub[1] + 1) % R
+    assert not PR.verify_with_oracle_vk(opk, 8, pub, a, b, cc)
     O.lib().oracle_pk_free(opk)
