@@ -199,6 +199,23 @@ int zkmi_groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1c
 int zkmi_pk_synthetic(zkmi_ctx* ctx, uint64_t seed, uint32_t log_n, size_t num_instance, size_t num_witness,
                       zkmi_pk** out);
 
+/* Groth16 circuit-specific setup on the GPU.  Replaces
+ * Groth16::<Bn254>::circuit_specific_setup (prover/src/bin/keygen.rs:87-91,
+ * ark-groth16 0.5 generate_parameters_with_qap): QAP evaluation at t over the
+ * radix-2 domain, then every query point as a fixed-base multiple of the
+ * generators.  The caller draws the randomness in arkworks' order from its
+ * StdRng (alpha, beta, gamma, delta = Fr::rand; G1::rand; G2::rand; then
+ * t = Fr::rand until t^n != 1):
+ *   toxic = alpha | beta | gamma | delta | t   (5 x 4 u64, canonical Fr)
+ *   g1 (8 u64), g2 (16 u64)                     canonical affine generators
+ * The key is resident (as after zkmi_pk_load) and equals arkworks' key for
+ * the same inputs. */
+int zkmi_groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t toxic[20], const uint64_t g1[8],
+                       const uint64_t g2[16], zkmi_pk** out);
+/* ProvingKey::serialize_compressed of a resident key (keygen.rs:101-104);
+ * buf = NULL queries the length. */
+int zkmi_pk_serialize(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len);
+
 /* ------------------------------------------------------------- encodings */
 /* 256 B Solana layout: -A (x,y LE) || B (x.c0,x.c1,y.c0,y.c1 LE) || C (x,y LE)
  * (prover.rs:304-334) */

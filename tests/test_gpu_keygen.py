@@ -1,0 +1,131 @@
+"""GPU keygen (zkmi_groth16_setup, keygen.rs:87-91) parity.
+
+* SquareCircuit, StdRng(42): the GPU-built key serializes to exactly the
+  oracle's arkworks bytes, its VK reproduces the reference's l2_vk.json prefix,
+  and a proof with the continuing rng reproduces proof_for_onchain.json.
+* L2BlockCircuit::dummy() with seed 0 (the reference's keygen) and seeded
+  synthetic / zelana_batch circuits: GPU key bytes == oracle key bytes.
+* Config 4 end to end: the full batch-70 zelana_batch circuit (2^21 domain)
+  gets a GPU key, a GPU proof, and the proof VERIFIES (pairing check).
+"""
+import base64
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from zelana_amd.gpu import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _oracle_key(cs, seed):
+    st, keep = O.make_r1cs(cs)
+    rng = O.Rng(seed)
+    opk = O.lib().oracle_groth16_setup(ctypes.byref(st), rng.h, 8)
+    size = O.lib().oracle_pk_serialize(opk, 1, None, 0)
+    buf = np.zeros(size, np.uint8)
+    O.lib().oracle_pk_serialize(opk, 1, buf.ctypes.data, size)
+    return opk, buf.tobytes(), (st, keep, rng)
+
+
+def _gpu_key(ctx, cs, seed):
+    from zelana_amd.keygen import circuit_specific_setup
+    from zelana_amd.rng import StdRng
+    pk, vk = circuit_specific_setup(ctx, cs, StdRng.seed_from_u64(seed))
+    return pk, vk
+
+
+def test_square_circuit_key_and_proof(ctx):
+    from zelana_amd import gpu
+    from zelana_amd.keygen import setup_randomness
+    from zelana_amd.r1cs import square_circuit
+    from zelana_amd.rng import StdRng
+    cs, z = square_circuit(7)
+    opk, want, keep = _oracle_key(cs, 42)
+    toxic, g1, g2, rng = setup_randomness(StdRng.seed_from_u64(42), cs.num_constraints, cs.num_instance)
+    pk = gpu.ProvingKey.setup(ctx, cs, toxic, np.array(g1, np.uint64), np.array(g2, np.uint64))
+    assert pk.serialize() == want
+    ref_vk = base64.b64decode(json.load(open(os.path.join(GOLD, "ref_l2_vk.json")))["verifying_key"])
+    assert pk.vk_bytes()[:224] == ref_vk[:224]
+    r, s = rng.fr_rand(), rng.fr_rand()
+    zz = np.array([O.int_to_limbs(v) for v in z], np.uint64)
+    a, b, c = gpu.groth16_prove(ctx, pk, cs, zz, r, s)
+    ref = json.load(open(os.path.join(GOLD, "ref_proof_for_onchain.json")))["proof_components"]
+    for pt, name, ser in ((a, "pi_a", O.lib().oracle_g1_serialize), (b, "pi_b", O.lib().oracle_g2_serialize),
+                          (c, "pi_c", O.lib().oracle_g1_serialize)):
+        out = np.zeros(len(ref[name]), np.uint8)
+        ser(O.P(pt), 0, O.P(out))
+        assert list(out) == ref[name], name
+    O.lib().oracle_pk_free(opk)
+
+
+def test_l2block_keygen_seed0_matches_oracle(ctx):
+    """prover/src/bin/keygen.rs: StdRng(0) over L2BlockCircuit::dummy()."""
+    from zelana_amd.l2block import L2BlockCircuit
+    cs, _, _ = L2BlockCircuit.dummy().synthesize()
+    opk, want, keep = _oracle_key(cs, 0)
+    pk, vk = _gpu_key(ctx, cs, 0)
+    got = pk.serialize()
+    assert len(got) == len(want) and got == want
+    assert got[:len(vk)] == vk
+    O.lib().oracle_pk_free(opk)
+
+
+@pytest.mark.parametrize("m,l,w,seed", [(300, 3, 500, 1), (5000, 9, 4100, 2)])
+def test_synthetic_keygen_matches_oracle(ctx, m, l, w, seed):
+    from zelana_amd.r1cs import synthetic
+    cs, _ = synthetic(m, l, w, seed=seed, satisfied=False)
+    opk, want, keep = _oracle_key(cs, seed)
+    pk, _ = _gpu_key(ctx, cs, seed)
+    assert pk.serialize() == want
+    O.lib().oracle_pk_free(opk)
+
+
+def test_zbatch_full_keygen_prove_verify(ctx):
+    """Config 4 with a real key: batch 70 of forge/circuits/zelana_batch
+    (Prover.toml), GPU keygen (seed 0), GPU proof with r, s from
+    StdRng(batch_id), pairing check against the key's VK."""
+    import pairing as PR
+    from zelana_amd import gpu, zbatch
+    from zelana_amd.rng import StdRng
+    d = zbatch.load_prover_toml(os.path.join(GOLD, "zelana_batch_70_Prover.toml"))
+    cs, z, _ = zbatch.build(d)
+    pk, vk = _gpu_key(ctx, cs, 0)
+    pk.precompute()
+    rng = StdRng.seed_from_u64(int(d["batch_id"]))
+    r, s = rng.fr_rand(), rng.fr_rand()
+    a, b, c = gpu.groth16_prove(ctx, pk, cs, z, r, s)
+    pub = [O.limbs_to_int(z[i]) for i in range(1, cs.num_instance)]
+    vkd = _vk_points(vk, cs.num_instance)
+    g1_add, g1_mul = PR.oracle_g1_ops()
+    assert PR.groth16_verify(vkd, pub, a, b, c, g1_add, g1_mul)
+    pub[1] = (pub[1] + 1) % O.R
+    assert not PR.groth16_verify(vkd, pub, a, b, c, g1_add, g1_mul)
+
+
+def _vk_points(vk: bytes, num_instance: int):
+    """compressed arkworks VK -> canonical points (oracle decoder)."""
+    def g1(off):
+        out = np.zeros(8, np.uint64)
+        assert O.lib().oracle_g1_deserialize(O.P(np.frombuffer(vk[off:off + 32], np.uint8).copy()), 1, O.P(out)) == 1
+        return out
+
+    def g2(off):
+        out = np.zeros(16, np.uint64)
+        assert O.lib().oracle_g2_deserialize(O.P(np.frombuffer(vk[off:off + 64], np.uint8).copy()), 1, O.P(out)) == 1
+        return out
+    assert int.from_bytes(vk[224:232], "little") == num_instance
+    return {"alpha": g1(0), "beta": g2(32), "gamma": g2(96), "delta": g2(160),
+            "ic": [g1(232 + 32 * i) for i in range(num_instance)]}

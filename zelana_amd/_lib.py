@@ -83,6 +83,8 @@ SIGNATURES = [
     ("zkmi_r1cs_destroy", None, [vp]),
     ("zkmi_groth16_prove_resident", ctypes.c_int, [vp, vp, vp, vp, u64p, u64p, u64p, u64p, u64p]),
     ("zkmi_pk_synthetic", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint32, sz, sz, ctypes.POINTER(vp)]),
+    ("zkmi_groth16_setup", ctypes.c_int, [vp, vp, u64p, u64p, u64p, ctypes.POINTER(vp)]),
+    ("zkmi_pk_serialize", ctypes.c_int, [vp, u8p, sz, ctypes.POINTER(sz)]),
     ("zkmi_proof_to_solana_bytes", ctypes.c_int, [u64p, u64p, u64p, u8p]),
     ("zkmi_proof_serialize_compressed", ctypes.c_int, [u64p, u64p, u64p, u8p]),
 ]

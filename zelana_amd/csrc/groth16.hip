@@ -778,6 +778,252 @@ int pk_synthetic(zkmi_ctx* ctx, uint64_t seed, uint32_t log_n, size_t l, size_t 
   return 0;
 }
 
+// ------------------------------------------------------------ setup
+// Groth16::circuit_specific_setup (keygen.rs:87-91) = ark-groth16 0.5
+// generate_parameters_with_qap with LibsnarkReduction::instance_map_with_
+// evaluation: Lagrange values u_i = L_i(t) over the radix-2 domain, column
+// sums a_j(t) = sum_i A[i][j] u_i (+ u_{m+j} for the instance rows of A),
+// then every query point is a scalar multiple of the G1 / G2 generator
+// (fixed_base_mul).  Field results are exact, group results are exact, so the
+// key equals arkworks' for the same toxic waste and generators.
+__constant__ uint32_t SETUP_W28[8] = {0x725b19f0u, 0x9bd61b6eu, 0x41112ed4u, 0x402d111eu,
+                                      0x8ef62abcu, 0x00e0a7ebu, 0xa58a7e85u, 0x2a3c09f0u};
+__constant__ uint64_t SETUP_RM2[4] = {0x43e1f593efffffffull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
+                                      0x30644e72e131a029ull};  // r - 2
+enum { SC_ALPHA, SC_BETA, SC_GINV, SC_DINV, SC_T, SC_OMEGA, SC_ZTN, SC_ZTD, SC_COUNT };
+// tw: alpha, beta, gamma, delta, t (canonical); out: Montgomery constants
+__global__ void k_setup_consts(const uint32_t* __restrict__ tw, uint32_t logn, uint32_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const uint64_t rm2[4] = {SETUP_RM2[0], SETUP_RM2[1], SETUP_RM2[2], SETUP_RM2[3]};
+  Fe a = to_mont<FrP>(ld_fe(tw)), b = to_mont<FrP>(ld_fe(tw + 8)), g = to_mont<FrP>(ld_fe(tw + 16)),
+     d = to_mont<FrP>(ld_fe(tw + 24)), t = to_mont<FrP>(ld_fe(tw + 32));
+  Fe w = to_mont<FrP>(ldc_fe(SETUP_W28));
+  for (uint32_t k = logn; k < 28; k++) w = sqr<FrP>(w);
+  Fe tn = t;
+  for (uint32_t k = 0; k < logn; k++) tn = sqr<FrP>(tn);
+  Fe zt = sub<FrP>(tn, one<FrP>());  // vanishing polynomial at t
+  Fe nn = one<FrP>();
+  for (uint32_t k = 0; k < logn; k++) nn = add<FrP>(nn, nn);
+  Fe di = pow<FrP>(d, rm2);
+  const Fe vals[SC_COUNT] = {a, b, pow<FrP>(g, rm2), di, t, w, mul<FrP>(zt, pow<FrP>(nn, rm2)), mul<FrP>(zt, di)};
+  for (int k = 0; k < SC_COUNT; k++) st_fe(out + 8 * k, reduce<FrP>(vals[k]));
+}
+// u_i = L_i(t) = Z(t) omega^i / (n (t - omega^i)), Montgomery (evaluate_all_lagrange_coefficients)
+__global__ void __launch_bounds__(256) k_setup_lagrange(const uint32_t* __restrict__ sc, size_t n,
+                                                        uint32_t* __restrict__ u) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t rm2[4] = {SETUP_RM2[0], SETUP_RM2[1], SETUP_RM2[2], SETUP_RM2[3]};
+  const uint64_t e[4] = {(uint64_t)i, 0, 0, 0};
+  const Fe w = pow<FrP>(ld_fe(sc + 8 * SC_OMEGA), e);
+  const Fe inv = pow<FrP>(sub<FrP>(ld_fe(sc + 8 * SC_T), w), rm2);
+  st_fe(u + i * 8, reduce<FrP>(mul<FrP>(mul<FrP>(ld_fe(sc + 8 * SC_ZTN), w), inv)));
+}
+// column sums over a CSC matrix: out_j = sum_k val_k u_{row_k} (+ u_{m+j} for
+// j < l in A), canonical value form
+__global__ void __launch_bounds__(256) k_setup_cols(const uint64_t* __restrict__ colptr,
+                                                    const uint32_t* __restrict__ row, const uint32_t* __restrict__ val,
+                                                    const uint32_t* __restrict__ u, size_t m, size_t l, size_t nv,
+                                                    int is_a, uint32_t* __restrict__ out) {
+  const size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (j >= nv) return;
+  Fe acc = fe_zero();
+  for (uint64_t k = colptr[j]; k < colptr[j + 1]; k++) acc = add<FrP>(acc, mul<FrP>(ld_fe(val + k * 8), ld_fe(u + (size_t)row[k] * 8)));
+  if (is_a && j < l) acc = add<FrP>(acc, mul<FrP>(ld_fe(u + (m + j) * 8), Fe{{1, 0, 0, 0, 0, 0, 0, 0, 0}}));
+  st_fe(out + j * 8, reduce<FrP>(acc));
+}
+// gamma_abc (j < l): (beta a_j + alpha b_j + c_j) / gamma; l_query (j >= l): the same / delta
+__global__ void __launch_bounds__(256) k_setup_lscalars(const uint32_t* __restrict__ va, const uint32_t* __restrict__ vb,
+                                                        const uint32_t* __restrict__ vc, const uint32_t* __restrict__ sc,
+                                                        size_t l, size_t nv, uint32_t* __restrict__ abc,
+                                                        uint32_t* __restrict__ lq) {
+  const size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (j >= nv) return;
+  Fe k = add<FrP>(add<FrP>(mul<FrP>(ld_fe(va + j * 8), ld_fe(sc + 8 * SC_BETA)),
+                           mul<FrP>(ld_fe(vb + j * 8), ld_fe(sc + 8 * SC_ALPHA))),
+                  ld_fe(vc + j * 8));
+  Fe v = reduce<FrP>(mul<FrP>(k, ld_fe(sc + 8 * (j < l ? SC_GINV : SC_DINV))));
+  if (j < l) st_fe(abc + j * 8, v);
+  else st_fe(lq + (j - l) * 8, v);
+}
+// h_query scalars Z(t) t^i / delta (h_query_scalars), stored at position p with
+// i = rev(p): the resident key keeps h bit-reversed (see decode_to_bases)
+__global__ void __launch_bounds__(256) k_setup_h(const uint32_t* __restrict__ sc, uint32_t logn, size_t cnt,
+                                                 uint32_t* __restrict__ out) {
+  const size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (p >= cnt) return;
+  const uint64_t e[4] = {logn ? (uint64_t)(__brev((uint32_t)p) >> (32 - logn)) : 0, 0, 0, 0};
+  st_fe(out + p * 8, from_mont<FrP>(mul<FrP>(pow<FrP>(ld_fe(sc + 8 * SC_T), e), ld_fe(sc + 8 * SC_ZTD))));
+}
+
+// host CSR -> CSC (column pointers u64, row indices u32, 32-B coefficients)
+static void csr_to_csc(const uint64_t* rp, const uint64_t* col, const uint64_t* val, size_t m, size_t nv,
+                       std::vector<uint64_t>& cp, std::vector<uint32_t>& rows, std::vector<uint64_t>& vals) {
+  const uint64_t nnz = rp[m];
+  cp.assign(nv + 1, 0);
+  for (uint64_t k = 0; k < nnz; k++) cp[col[k] + 1]++;
+  for (size_t j = 0; j < nv; j++) cp[j + 1] += cp[j];
+  std::vector<uint64_t> cur(cp.begin(), cp.end() - 1);
+  rows.resize(std::max<uint64_t>(1, nnz));
+  vals.resize(std::max<uint64_t>(1, nnz) * 4);
+  for (size_t i = 0; i < m; i++)
+    for (uint64_t k = rp[i]; k < rp[i + 1]; k++) {
+      const uint64_t d = cur[col[k]]++;
+      rows[d] = (uint32_t)i;
+      memcpy(&vals[d * 4], &val[k * 4], 32);
+    }
+}
+
+int groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t tw[20], const uint64_t g1[8],
+                  const uint64_t g2[16], zkmi_pk** out) {
+  *out = nullptr;
+  ZK_TRY(check_cs(cs));
+  const size_t m = cs->num_constraints, l = cs->num_instance, w = cs->num_witness, nv = l + w;
+  const uint32_t logn = domain_log(m + l);
+  if (logn > 28 || m >= (1ull << 32)) {
+    set_error("setup: domain 2^%u exceeds Fr two-adicity", logn);
+    return ZKMI_EINVAL;
+  }
+  const size_t n = (size_t)1 << logn;
+  hipStream_t st = ctx->stream;
+  DevR1CS chk;
+  ZK_TRY(upload_r1cs(ctx, cs, &chk));  // validation only (shapes, column range)
+  uint32_t *d_tw, *d_sc, *u, *va, *vb, *vc, *abc, *lsc, *hs, *small, *pts;
+  ZK_TRY(ctx->ws.get("setup_tw", 5 * 32, (void**)&d_tw));
+  ZK_TRY(ctx->ws.get("setup_consts", SC_COUNT * 32, (void**)&d_sc));
+  ZK_TRY(ctx->ws.get("setup_u", n * 32, (void**)&u));
+  ZK_TRY(ctx->ws.get("setup_va", nv * 32, (void**)&va));
+  ZK_TRY(ctx->ws.get("setup_vb", nv * 32, (void**)&vb));
+  ZK_TRY(ctx->ws.get("setup_vc", nv * 32, (void**)&vc));
+  ZK_TRY(ctx->ws.get("setup_abc", l * 32 + 3 * 32, (void**)&abc));
+  ZK_TRY(ctx->ws.get("setup_l", std::max<size_t>(1, w) * 32, (void**)&lsc));
+  ZK_TRY(ctx->ws.get("setup_h", n * 32, (void**)&hs));
+  ZK_TRY(ctx->ws.get("setup_small", (l + 6) * 32, (void**)&small));
+  ZK_TRY(ctx->ws.get("setup_pts", std::max(nv, n) * 128, (void**)&pts));
+  ZK_HIP(hipMemcpyAsync(d_tw, tw, 5 * 32, hipMemcpyHostToDevice, st));
+  k_setup_consts<<<1, 64, 0, st>>>(d_tw, logn, d_sc);
+  k_setup_lagrange<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d_sc, n, u);
+  const uint64_t* rps[3] = {cs->a_rowptr, cs->b_rowptr, cs->c_rowptr};
+  const uint64_t* cols[3] = {cs->a_col, cs->b_col, cs->c_col};
+  const uint64_t* vals[3] = {cs->a_val, cs->b_val, cs->c_val};
+  uint32_t* outs[3] = {va, vb, vc};
+  for (int t = 0; t < 3; t++) {
+    std::vector<uint64_t> cp, cv;
+    std::vector<uint32_t> rows;
+    csr_to_csc(rps[t], cols[t], vals[t], m, nv, cp, rows, cv);
+    uint64_t* d_cp;
+    uint32_t *d_rows, *d_val;
+    ZK_TRY(ctx->ws.get("setup_cp", cp.size() * 8, (void**)&d_cp));
+    ZK_TRY(ctx->ws.get("setup_rows", rows.size() * 4, (void**)&d_rows));
+    ZK_TRY(ctx->ws.get("setup_cval", cv.size() * 8, (void**)&d_val));
+    ZK_HIP(hipMemcpyAsync(d_cp, cp.data(), cp.size() * 8, hipMemcpyHostToDevice, st));
+    ZK_HIP(hipMemcpyAsync(d_rows, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, st));
+    ZK_HIP(hipMemcpyAsync(d_val, cv.data(), cv.size() * 8, hipMemcpyHostToDevice, st));
+    k_setup_cols<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(d_cp, d_rows, d_val, u, m, l, nv, t == 0, outs[t]);
+    ZK_HIP(hipStreamSynchronize(st));  // host vectors die with this iteration
+  }
+  k_setup_lscalars<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(va, vb, vc, d_sc, l, nv, abc + 3 * 8, lsc);
+  k_setup_h<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d_sc, logn, n - 1, hs);
+  ZK_HIP(hipGetLastError());
+  // small G1 batch [alpha, beta, delta, gamma_abc...], G2 batch [beta, gamma, delta]
+  ZK_HIP(hipMemcpyAsync(abc, tw, 64, hipMemcpyHostToDevice, st));
+  ZK_HIP(hipMemcpyAsync(abc + 16, tw + 12, 32, hipMemcpyHostToDevice, st));
+  ZK_HIP(hipMemcpyAsync(small, tw + 4, 96, hipMemcpyHostToDevice, st));
+  zkmi_pk* pk = new zkmi_pk;
+  pk->ctx = ctx;
+  pk->n = n;
+  pk->log_n = logn;
+  pk->num_instance = l;
+  pk->num_witness = w;
+  int rc = 0;
+  auto fail = [&](int code) {
+    zkmi_pk_destroy(pk);
+    return code;
+  };
+  std::vector<uint64_t> s1((3 + l) * 8), s2(3 * 16);
+  if ((rc = fixed_base_mul(ctx, 0, g1, abc, 3 + l, pts))) return fail(rc);
+  if (hipMemcpy(s1.data(), pts, s1.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return fail(ZKMI_EHIP);
+  if ((rc = fixed_base_mul(ctx, 1, g2, small, 3, pts))) return fail(rc);
+  if (hipMemcpy(s2.data(), pts, s2.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return fail(ZKMI_EHIP);
+  memcpy(pk->alpha_g1, &s1[0], 64);
+  memcpy(pk->beta_g1, &s1[8], 64);
+  memcpy(pk->delta_g1, &s1[16], 64);
+  pk->gamma_abc.assign(s1.begin() + 24, s1.end());
+  memcpy(pk->beta_g2, &s2[0], 128);
+  memcpy(pk->gamma_g2, &s2[16], 128);
+  memcpy(pk->delta_g2, &s2[32], 128);
+  struct Q {
+    int g2;
+    const uint32_t* sc;
+    size_t cnt;
+    zkmi_bases** dst;
+    uint64_t* first;
+  } qs[5] = {{0, va, nv, &pk->a_query, pk->a0},
+             {0, vb, nv, &pk->b_g1_query, pk->b1_0},
+             {1, vb, nv, &pk->b_g2_query, pk->b2_0},
+             {0, hs, n - 1, &pk->h_query_rev, nullptr},
+             {0, lsc, w, &pk->l_query, nullptr}};
+  for (const Q& q : qs) {
+    if ((rc = fixed_base_mul(ctx, q.g2, q.g2 ? g2 : g1, q.sc, q.cnt, pts))) return fail(rc);
+    if (q.first && hipMemcpy(q.first, pts, q.g2 ? 128 : 64, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(ZKMI_EHIP);
+    if ((rc = bases_from_device_canon(ctx, q.g2, pts, q.cnt, q.dst))) return fail(rc);
+  }
+  std::vector<uint8_t> v(32 + 3 * 64 + 8 + l * 32);
+  g1_compress(pk->alpha_g1, v.data());
+  g2_compress(pk->beta_g2, v.data() + 32);
+  g2_compress(pk->gamma_g2, v.data() + 96);
+  g2_compress(pk->delta_g2, v.data() + 160);
+  for (int i = 0; i < 8; i++) v[224 + i] = (uint8_t)((uint64_t)l >> (8 * i));
+  for (size_t i = 0; i < l; i++) g1_compress(&pk->gamma_abc[i * 8], v.data() + 232 + i * 32);
+  pk->vk_compressed = v;
+  if ((rc = timer_flush(ctx))) return fail(rc);
+  *out = pk;
+  return 0;
+}
+
+// ProvingKey::serialize_compressed (keygen.rs:103): vk | beta_g1 | delta_g1 |
+// a | b_g1 | b_g2 | h | l, each query a u64 length then points
+int pk_serialize(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {
+  const size_t nv = pk->num_instance + pk->num_witness, nh = pk->n - 1, nl = pk->num_witness;
+  const size_t total = pk->vk_compressed.size() + 64 + (8 + 32 * nv) * 2 + (8 + 64 * nv) + (8 + 32 * nh) + (8 + 32 * nl);
+  *len = total;
+  if (!buf) return 0;
+  if (cap < total) {
+    set_error("pk_serialize: buffer of %zu bytes, need %zu", cap, total);
+    return ZKMI_EINVAL;
+  }
+  uint8_t* o = buf;
+  memcpy(o, pk->vk_compressed.data(), pk->vk_compressed.size());
+  o += pk->vk_compressed.size();
+  g1_compress(pk->beta_g1, o);
+  g1_compress(pk->delta_g1, o + 32);
+  o += 64;
+  auto put_len = [&](uint64_t k) {
+    for (int i = 0; i < 8; i++) o[i] = (uint8_t)(k >> (8 * i));
+    o += 8;
+  };
+  auto put_query = [&](const zkmi_bases* b, size_t cnt, bool rev) -> int {
+    const int pw = b->g2 ? 16 : 8;
+    std::vector<uint64_t> pts(std::max<size_t>(1, b->n) * pw);
+    ZK_TRY(bases_export(b, pts.data()));
+    put_len(cnt);
+    for (size_t i = 0; i < cnt; i++) {
+      size_t src = i;
+      if (rev) src = pk->log_n ? (__builtin_bitreverse32((uint32_t)i) >> (32 - pk->log_n)) : 0;
+      if (b->g2) g2_compress(&pts[src * pw], o), o += 64;
+      else g1_compress(&pts[src * pw], o), o += 32;
+    }
+    return 0;
+  };
+  ZK_TRY(put_query(pk->a_query, nv, false));
+  ZK_TRY(put_query(pk->b_g1_query, nv, false));
+  ZK_TRY(put_query(pk->b_g2_query, nv, false));
+  ZK_TRY(put_query(pk->h_query_rev, nh, true));
+  ZK_TRY(put_query(pk->l_query, nl, false));
+  return 0;
+}
+
 }  // namespace zk
 
 using namespace zk;
@@ -867,5 +1113,20 @@ int zkmi_groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, co
   int rc = groth16_prove(ctx, pk, cs, z, r, s, a_out, b_out, c_out);
   if (rc == 0) rc = timer_flush(ctx);
   return rc;
+}
+int zkmi_groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t toxic[20], const uint64_t g1[8],
+                       const uint64_t g2[16], zkmi_pk** out) {
+  if (!ctx || !cs || !toxic || !g1 || !g2 || !out) {
+    set_error("zkmi_groth16_setup: null argument");
+    return ZKMI_EINVAL;
+  }
+  return groth16_setup(ctx, cs, toxic, g1, g2, out);
+}
+int zkmi_pk_serialize(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {
+  if (!pk || !len) {
+    set_error("zkmi_pk_serialize: null argument");
+    return ZKMI_EINVAL;
+  }
+  return pk_serialize(pk, buf, cap, len);
 }
 }  // extern "C"

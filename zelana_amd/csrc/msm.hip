@@ -1254,6 +1254,106 @@ __global__ void __launch_bounds__(256) k_bases_table(uint32_t* __restrict__ pts,
   }
 }
 
+// ------------------------------------------------- fixed-base scalar mult
+// k_i * G for a batch of scalars and ONE base (Groth16 setup: every query
+// point is a multiple of the G1 / G2 generator, ark-groth16 FixedBase::msm).
+// Table: window w (8 bits, 32 windows cover 256 bits) entry d = d 2^(8w) G,
+// internal affine.  A scalar then costs <= 32 mixed additions and one
+// inversion (of ZZ * ZZZ) to come back to affine.
+constexpr int FB_WIN = 8, FB_NW = 32;
+template <class G>
+__global__ void __launch_bounds__(256) k_fb_table(const uint32_t* __restrict__ gen, uint32_t* __restrict__ tab) {
+  using F = typename G::F;
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (uint32_t)FB_NW << FB_WIN) return;
+  const uint32_t w = e >> FB_WIN, d = e & ((1u << FB_WIN) - 1);
+  uint32_t* o = tab + (size_t)e * G::PW;
+  if (d == 0) {
+    for (int k = 0; k < G::PW; k++) o[k] = 0;
+    o[G::PW - 1] = 0x80000000u;
+    return;
+  }
+  const Aff<F> g = ld_aff<G>(gen, 0);
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (int b = FB_WIN - 1; b >= 0; b--) {
+    acc = xyzz_dbl(acc);
+    if ((d >> b) & 1) acc = xyzz_madd(acc, g);
+  }
+  for (uint32_t k = 0; k < FB_WIN * w; k++) acc = xyzz_dbl(acc);
+  auto t = inv_any<F>(F::mul(acc.zz, acc.zzz));
+  Aff<F> q;
+  q.x = F::mul(acc.x, F::mul(t, acc.zzz));
+  q.y = F::mul(acc.y, F::mul(t, acc.zz));
+  if constexpr (G::CW == 8) {
+    st_fe(o, reduce<FqP>(q.x));
+    st_fe(o + 8, reduce<FqP>(q.y));
+  } else {
+    st_fe(o, reduce<FqP>(q.x.c0));
+    st_fe(o + 8, reduce<FqP>(q.x.c1));
+    st_fe(o + 16, reduce<FqP>(q.y.c0));
+    st_fe(o + 24, reduce<FqP>(q.y.c1));
+  }
+}
+// out[i] = scalars[i] * G, canonical affine (all-zero = infinity); scalars
+// canonical packed 8 x u32, < r.
+template <class G>
+__global__ void __launch_bounds__(256) k_fb_mul(const uint32_t* __restrict__ tab, const uint32_t* __restrict__ sc,
+                                                size_t n, uint32_t* __restrict__ out) {
+  using F = typename G::F;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 a = reinterpret_cast<const uint4*>(sc)[2 * i], b = reinterpret_cast<const uint4*>(sc)[2 * i + 1];
+  const uint32_t s[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (int w = 0; w < FB_NW; w++) {
+    const uint32_t d = (s[w >> 2] >> (8 * (w & 3))) & 0xFFu;
+    if (d) acc = xyzz_madd(acc, ld_aff<G>(tab, (uint32_t)(w << FB_WIN) + d));
+  }
+  uint32_t* q = out + i * G::PW;
+  if (xyzz_is_inf(acc)) {
+    for (int k = 0; k < G::PW; k++) q[k] = 0;
+    return;
+  }
+  auto t = inv_any<F>(F::mul(acc.zz, acc.zzz));
+  Aff<F> r;
+  r.x = F::mul(acc.x, F::mul(t, acc.zzz));
+  r.y = F::mul(acc.y, F::mul(t, acc.zz));
+  if constexpr (G::CW == 8) {
+    st_fe(q, from_mont<FqP>(r.x));
+    st_fe(q + 8, from_mont<FqP>(r.y));
+  } else {
+    st_fe(q, from_mont<FqP>(r.x.c0));
+    st_fe(q + 8, from_mont<FqP>(r.x.c1));
+    st_fe(q + 16, from_mont<FqP>(r.y.c0));
+    st_fe(q + 24, from_mont<FqP>(r.y.c1));
+  }
+}
+
+// host: d_out[i] = d_scalars[i] * gen (gen canonical affine on the host)
+int fixed_base_mul(zkmi_ctx* ctx, int g2, const uint64_t* gen, const uint32_t* d_scalars, size_t n,
+                   uint32_t* d_out) {
+  zkmi_bases* gb = nullptr;
+  ZK_TRY(bases_upload(ctx, g2, gen, 1, &gb));  // validates the generator (on the curve)
+  const int pw = g2 ? 32 : 16;
+  uint32_t* tab;
+  int rc = ctx->ws.get(g2 ? "fb_table_g2" : "fb_table_g1", (size_t)(FB_NW << FB_WIN) * pw * 4, (void**)&tab);
+  if (!rc) {
+    const unsigned gt = (unsigned)(((FB_NW << FB_WIN) + 255) / 256), gm = (unsigned)((n + 255) / 256);
+    if (g2) k_fb_table<G2T><<<gt, 256, 0, ctx->stream>>>(gb->d_pts, tab);
+    else k_fb_table<G1T><<<gt, 256, 0, ctx->stream>>>(gb->d_pts, tab);
+    if (n) {
+      if (g2) k_fb_mul<G2T><<<gm, 256, 0, ctx->stream>>>(tab, d_scalars, n, d_out);
+      else k_fb_mul<G1T><<<gm, 256, 0, ctx->stream>>>(tab, d_scalars, n, d_out);
+    }
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      set_error("fixed_base_mul: kernel failure");
+      rc = ZKMI_EHIP;
+    }
+  }
+  zkmi_bases_destroy(gb);
+  return rc;
+}
+
 // internal -> canonical affine (export for checking)
 template <class G>
 __global__ void __launch_bounds__(256) k_bases_export(const uint32_t* __restrict__ in, size_t n,

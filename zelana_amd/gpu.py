@@ -245,6 +245,33 @@ class ProvingKey:
         check(lib().zkmi_pk_vk_bytes(self.h, buf.ctypes.data_as(u8p), ln.value, ctypes.byref(ln)))
         return buf.tobytes()
 
+    def serialize(self) -> bytes:
+        """ProvingKey::serialize_compressed (zkmi_pk_serialize)."""
+        ln = ctypes.c_size_t()
+        check(lib().zkmi_pk_serialize(self.h, None, 0, ctypes.byref(ln)), "zkmi_pk_serialize")
+        buf = np.zeros(ln.value, np.uint8)
+        check(lib().zkmi_pk_serialize(self.h, buf.ctypes.data_as(u8p), ln.value, ctypes.byref(ln)),
+              "zkmi_pk_serialize")
+        return buf.tobytes()
+
+    @classmethod
+    def setup(cls, ctx: "Context", cs, toxic: list[int], g1, g2) -> "ProvingKey":
+        """zkmi_groth16_setup: toxic = [alpha, beta, gamma, delta, t], g1 / g2
+        canonical affine generators (see zelana_amd/keygen.py for the RNG)."""
+        st, keep = r1cs_struct(cs)
+        tw = np.concatenate([_limbs(v) for v in toxic])
+        pk = cls.__new__(cls)
+        pk.ctx = ctx
+        pk.h = vp()
+        check(lib().zkmi_groth16_setup(ctx.h, ctypes.byref(st), _p64(tw), _p64(np.ascontiguousarray(g1, np.uint64)),
+                                       _p64(np.ascontiguousarray(g2, np.uint64)), ctypes.byref(pk.h)),
+              "zkmi_groth16_setup")
+        del keep
+        info = np.zeros(3, np.uint64)
+        check(lib().zkmi_pk_info(pk.h, _p64(info)))
+        pk.n, pk.num_instance, pk.num_witness = (int(x) for x in info)
+        return pk
+
     def close(self):
         if self.h:
             lib().zkmi_pk_destroy(self.h)
