@@ -83,6 +83,22 @@ def test_l2block_keygen_seed0_matches_oracle(ctx):
     O.lib().oracle_pk_free(opk)
 
 
+def test_prover_keygen_roundtrip():
+    """Groth16Prover.keygen (keygen.rs) -> bytes -> Groth16Prover.from_bytes:
+    the loaded key proves the same as the generated one, and the VK hash is
+    blake3 of the compressed VK (prover.rs:289-294)."""
+    from zelana_amd.blake3 import blake3
+    from zelana_amd.prover import AccountStateSnapshot, BatchPublicInputs, BatchWitness, Groth16Prover, Transfer
+    p1, pkb, vkb = Groth16Prover.keygen(seed=0)
+    p2 = Groth16Prover.from_bytes(pkb, vkb)
+    assert p1.verification_key_hash() == p2.verification_key_hash() == blake3(vkb)
+    snd, rcv = bytes([1] * 32), bytes([2] * 32)
+    w = BatchWitness(transactions=[Transfer(snd, rcv, 100)],
+                     pre_account_states=[AccountStateSnapshot(snd, 1000), AccountStateSnapshot(rcv, 0)])
+    inp = BatchPublicInputs(batch_id=9)
+    assert p1.prove(inp, w).proof_bytes == p2.prove(inp, w).proof_bytes
+
+
 @pytest.mark.parametrize("m,l,w,seed", [(300, 3, 500, 1), (5000, 9, 4100, 2)])
 def test_synthetic_keygen_matches_oracle(ctx, m, l, w, seed):
     from zelana_amd.r1cs import synthetic

@@ -141,6 +141,22 @@ class Groth16Prover:
         return cls(ctx, pk, vk_bytes, circuit)
 
     @classmethod
+    def keygen(cls, device: int = 0, seed: int = 0, circuit_shape=None, precompute: bool = True):
+        """prover/src/bin/keygen.rs: Groth16::circuit_specific_setup(L2BlockCircuit::dummy(),
+        StdRng::seed_from_u64(seed)) with the key built on the GPU.  Returns
+        (prover, pk_bytes, vk_bytes); the bytes are arkworks' serialize_compressed."""
+        from .keygen import circuit_specific_setup
+        from .l2block import L2BlockCircuit
+
+        ctx = gpu.Context(device)
+        cs, _, _ = (circuit_shape or L2BlockCircuit.dummy()).synthesize()
+        pk, vk = circuit_specific_setup(ctx, cs, StdRng.seed_from_u64(seed))
+        pk_bytes = pk.serialize()
+        if precompute:
+            pk.precompute()
+        return cls(ctx, pk, vk), pk_bytes, vk
+
+    @classmethod
     def from_files(cls, pk_path: str, vk_path: str, **kw):
         with open(pk_path, "rb") as f:
             pkb = f.read()
