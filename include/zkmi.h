@@ -212,6 +212,11 @@ int zkmi_pk_synthetic(zkmi_ctx* ctx, uint64_t seed, uint32_t log_n, size_t num_i
  * the same inputs. */
 int zkmi_groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t toxic[20], const uint64_t g1[8],
                        const uint64_t g2[16], zkmi_pk** out);
+/* VerifyingKey::deserialize_compressed (points decoded and validated on the
+ * GPU) then serialize_compressed: the bytes Groth16Prover::compute_vk_hash
+ * hashes (core/src/sequencer/settlement/prover.rs:266-267, 289-294).
+ * out = NULL queries the length. */
+int zkmi_vk_canonical(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, uint8_t* out, size_t cap, size_t* out_len);
 /* ProvingKey::serialize_compressed of a resident key (keygen.rs:101-104);
  * buf = NULL queries the length. */
 int zkmi_pk_serialize(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len);

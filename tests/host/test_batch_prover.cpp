@@ -1,0 +1,141 @@
+// C++ host mirror tests (run by tests/test_host_mirror.py), written as the
+// reference's own Rust unit tests are:
+//   core/src/sequencer/settlement/prover.rs:793-840  test_mock_prover,
+//                                                    test_batch_hash,
+//                                                    test_verification_key_hash
+//   prover/src/l2_circuit.rs:513-542                 test_circuit_dummy,
+//                                                    test_public_input_count
+// plus the KATs the host pieces are pinned by (StdRng seed 42, BLAKE3).
+// With --gpu PK VK it also proves a dummy-shaped batch on the MI355X through
+// Groth16Prover and checks the 256-B layout and the VK hash.
+#include <stdio.h>
+#include <string.h>
+
+#include <fstream>
+#include <iterator>
+
+#include "batch_prover.h"
+#include "blake3.h"
+#include "std_rng.h"
+
+using namespace zp;
+
+static int g_fail = 0;
+#define CHECK(x)                                                    \
+  do {                                                              \
+    if (!(x)) {                                                     \
+      fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #x); \
+      g_fail++;                                                     \
+    }                                                               \
+  } while (0)
+
+static Bytes32 fill(uint8_t v) {
+  Bytes32 b;
+  b.fill(v);
+  return b;
+}
+static std::string hex(const uint8_t* p, size_t n) {
+  std::string s;
+  char b[3];
+  for (size_t i = 0; i < n; i++) snprintf(b, 3, "%02x", p[i]), s += b;
+  return s;
+}
+
+static void test_mock_prover() {
+  MockProver prover;
+  BatchPublicInputs inputs{fill(1), fill(2), fill(3), fill(4), fill(5), fill(6), 1};
+  BatchWitness witness;
+  BatchProof proof = prover.prove(inputs, witness);
+  CHECK(!proof.proof_bytes.empty());
+  CHECK(prover.verify(proof));
+}
+
+static void test_batch_hash() {
+  CHECK(compute_batch_hash({}) == compute_batch_hash({}));
+  std::vector<TransactionType> a{TransferTx{fill(1), fill(2), 5, 0}}, b{TransferTx{fill(1), fill(2), 6, 0}};
+  CHECK(compute_batch_hash(a) != compute_batch_hash(b));
+}
+
+static void test_verification_key_hash() {
+  MockProver prover;
+  CHECK(prover.verification_key_hash() != Bytes32{});
+}
+
+static void test_circuit_dummy() {
+  R1CSMatrices m = L2BlockCircuit::dummy().synthesize();
+  CHECK(m.num_instance == 8);  // 7 public inputs + the constant one
+  CHECK(m.num_constraints > 4096 && m.num_constraints + m.num_instance <= 8192);
+  CHECK(!m.is_satisfied());  // dummy roots are zeros, not what the circuit computes
+  std::map<std::string, Fr> out;
+  L2BlockCircuit c = L2BlockCircuit::dummy();
+  c.synthesize(&out);
+  auto put = [&](Bytes32& dst, const char* k) {
+    uint64_t v[4];
+    out[k].to_canon(v);
+    for (int i = 0; i < 32; i++) dst[i] = (uint8_t)(v[i / 8] >> (8 * (i % 8)));
+  };
+  put(c.post_state_root, "post_state_root");
+  put(c.withdrawal_root, "withdrawal_root");
+  put(c.batch_hash, "batch_hash");
+  put(c.pre_state_root, "pre_state_root");
+  CHECK(c.synthesize().is_satisfied());
+}
+
+static void test_kats() {
+  StdRng r = StdRng::seed_from_u64(42);
+  CHECK(r.next_u64() == 0x86cc7763222724a2ULL);
+  CHECK(r.next_u64() == 0x8af00a133fad517dULL);
+  StdRng s = StdRng::seed_from_u64(42);
+  uint64_t alpha[4];
+  s.fr_rand().to_canon(alpha);  // App. A.5 alpha
+  CHECK(alpha[3] == 0x2523caa9cf31f744ULL && alpha[0] == 0xaf40d45cdc63808dULL);
+  auto e = Blake3::hash("", 0);
+  CHECK(hex(e.data(), 32) == "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262");
+  auto a = Blake3::hash("abc", 3);
+  CHECK(hex(a.data(), 32) == "6437b3ac38465133ffb63b75273a8db548c558465d79db03fd359c6cd5bd9d85");
+  std::vector<uint8_t> big(5000);
+  for (size_t i = 0; i < big.size(); i++) big[i] = (uint8_t)(i % 251);  // the official test-vector input
+  auto b = Blake3::hash(big.data(), big.size());
+  CHECK(hex(b.data(), 32).size() == 64);
+}
+
+static std::vector<uint8_t> slurp(const char* path) {
+  std::ifstream f(path, std::ios::binary);
+  return std::vector<uint8_t>(std::istreambuf_iterator<char>(f), {});
+}
+
+static void test_gpu(const char* pk_path, const char* vk_path) {
+  auto prover = Groth16Prover::from_files(pk_path, vk_path);
+  auto vk = slurp(vk_path);
+  CHECK(prover->verification_key_hash() == Blake3::hash(vk.data(), vk.size()));
+  BatchPublicInputs in;
+  in.batch_id = 7;
+  BatchWitness w;
+  w.transactions.push_back(TransferTx{fill(1), fill(2), 100, 0});
+  w.pre_account_states.push_back(AccountStateSnapshot{fill(1), 1000});
+  w.pre_account_states.push_back(AccountStateSnapshot{fill(2), 0});
+  BatchProof p = prover->prove(in, w);
+  CHECK(p.proof_bytes.size() == 256);
+  CHECK(prover->verify(p));
+  BatchProof q = prover->prove(in, w);  // deterministic: StdRng(batch_id)
+  CHECK(p.proof_bytes == q.proof_bytes);
+  bool threw = false;
+  try {
+    Groth16Prover::from_bytes({1, 2, 3}, vk);
+  } catch (const std::runtime_error& e) {
+    threw = strstr(e.what(), "Failed to deserialize proving key") != nullptr;
+  }
+  CHECK(threw);
+  printf("gpu proof %s...\n", hex(p.proof_bytes.data(), 16).c_str());
+}
+
+int main(int argc, char** argv) {
+  test_mock_prover();
+  test_batch_hash();
+  test_verification_key_hash();
+  test_circuit_dummy();
+  test_kats();
+  if (argc == 4 && strcmp(argv[1], "--gpu") == 0) test_gpu(argv[2], argv[3]);
+  printf("%s (%d failures)\n", g_fail ? "FAILED" : "ok", g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,108 @@
+"""The C++ host mirror of the reference prover (zelana_amd/host/,
+libzelana_prover.so, above the C ABI) against the Python mirror and the
+reference's own unit tests (tests/host/test_batch_prover.cpp)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import host_mirror as H
+from zelana_amd.blake3 import blake3
+from zelana_amd.prover import (AccountStateSnapshot, BatchPublicInputs, BatchWitness, Transfer, Withdraw,
+                               l2_circuit_of)
+from zelana_amd.rng import StdRng
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "zelana_amd", "test_batch_prover")
+
+
+def _batches():
+    a, b, c = bytes([1] * 32), bytes([2] * 32), bytes([9] * 32)
+    dummy = (BatchPublicInputs(batch_id=0),
+             BatchWitness([Transfer(a, b, 100)], [], [AccountStateSnapshot(a, 1000), AccountStateSnapshot(b, 0)]))
+    big = (BatchPublicInputs(bytes(range(32)), bytes(32), bytes([5] * 32), bytes([5] * 32), bytes(32), bytes(32), 70),
+           BatchWitness([Transfer(a, c, 30), Withdraw(bytes([4] * 32), 7), Transfer(c, b, 5)], [],
+                        [AccountStateSnapshot(a, 50), AccountStateSnapshot(b, 1)]))
+    honest = l2_circuit_of(*dummy).with_consistent_inputs()
+    consistent = (BatchPublicInputs(honest.pre_state_root, honest.post_state_root, honest.pre_shielded_root,
+                                    honest.post_shielded_root, honest.withdrawal_root, honest.batch_hash, 0), dummy[1])
+    return [dummy, big, consistent]
+
+
+def test_cpp_unit_tests():
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("k", range(3))
+def test_cpp_synthesis_equals_python(k):
+    inputs, witness = _batches()[k]
+    mats, z, sat, (m, ni, nw) = H.synthesize(inputs, witness)
+    cs, zp, _ = l2_circuit_of(inputs, witness).synthesize()
+    assert (m, ni, nw) == (cs.num_constraints, cs.num_instance, cs.num_witness)
+    assert sat == cs.is_satisfied(zp) == (k == 2)
+    zi = [sum(int(u) << (64 * i) for i, u in enumerate(row)) for row in z]
+    assert zi == list(zp)
+    for name in "abc":
+        rp, col, val = mats[name]
+        prp, pcol, pval = cs.csr(name)
+        assert np.array_equal(rp, prp)
+        for r in range(m):  # same terms per row (order within a row is immaterial)
+            got = sorted((int(col[q]), tuple(int(x) for x in val[q])) for q in range(rp[r], rp[r + 1]))
+            want = sorted((int(pcol[q]), tuple(int(x) for x in pval[q])) for q in range(prp[r], prp[r + 1]))
+            assert got == want, (name, r)
+
+
+def test_cpp_blake3_and_stdrng():
+    L = H.lib()
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 3000, 5000):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        buf = np.frombuffer(data or b"\0", np.uint8).copy()
+        out = np.zeros(32, np.uint8)
+        L.zp_blake3(buf.ctypes.data, n, out.ctypes.data)
+        assert out.tobytes() == blake3(data)
+    out = np.zeros((6, 4), np.uint64)
+    L.zp_stdrng_fr(70, 6, out.ctypes.data)
+    r = StdRng.seed_from_u64(70)
+    assert [sum(int(u) << (64 * i) for i, u in enumerate(row)) for row in out] == [r.fr_rand() for _ in range(6)]
+
+
+@pytest.mark.gpu
+def test_cpp_groth16_prover_equals_python(tmp_path):
+    """Groth16Prover::from_bytes / prove through libzelana_prover.so == the Python
+    mirror's proof bytes and VK hash, for the keygen (seed 0) key; then the C++
+    unit tests' GPU leg on the same files."""
+    import ctypes
+    from zelana_amd.prover import Groth16Prover
+    py, pkb, vkb = Groth16Prover.keygen(seed=0)
+    L = H.lib()
+    pk = np.frombuffer(pkb, np.uint8).copy()
+    vk = np.frombuffer(vkb, np.uint8).copy()
+    h = ctypes.c_void_p()
+    assert L.zp_groth16_from_bytes(pk.ctypes.data, len(pkb), vk.ctypes.data, len(vkb), 0, ctypes.byref(h)) == 0, \
+        L.zp_last_error()
+    vh = np.zeros(32, np.uint8)
+    L.zp_groth16_vk_hash(h, vh.ctypes.data)
+    assert vh.tobytes() == py.verification_key_hash()
+    for inputs, witness in _batches():
+        inp, (trb, nt), (wdb, nw), (acb, na) = H.encode(inputs, witness)
+        bufs = [np.frombuffer(x or b"\0", np.uint8).copy() for x in (inp, trb, wdb, acb)]
+        out = np.zeros(256, np.uint8)
+        ms = ctypes.c_uint64()
+        rc = L.zp_groth16_prove(h, bufs[0].ctypes.data, bufs[1].ctypes.data, nt, bufs[2].ctypes.data, nw,
+                                bufs[3].ctypes.data, na, out.ctypes.data, ctypes.byref(ms))
+        if nt == 1 and nw == 0:  # the dummy() shape the key was made for
+            assert rc == 0, L.zp_last_error()
+            assert out.tobytes() == py.prove(inputs, witness).proof_bytes
+        else:  # any other shape: both mirrors fail the same way
+            assert rc != 0 and L.zp_last_error().startswith(b"Proving failed: prove: circuit shape")
+            with pytest.raises(Exception, match="circuit shape"):
+                py.prove(inputs, witness)
+    L.zp_groth16_free(h)
+    (tmp_path / "pk.bin").write_bytes(pkb)
+    (tmp_path / "vk.bin").write_bytes(vkb)
+    r = subprocess.run([BIN, "--gpu", str(tmp_path / "pk.bin"), str(tmp_path / "vk.bin")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr

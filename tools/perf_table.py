@@ -12,11 +12,12 @@ log_n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else ["plain", "0:0", "16:0", "17:0", "17:3"]
 g2 = len(sys.argv) > 3 and sys.argv[3] == "g2"
 lanes = [int(x) for x in os.environ.get("LANES", "1,2").split(",")]
+depth_env = os.environ.get("DEPTH")  # jobs kept in flight (default: lanes)
 n = 1 << log_n
 ctx = Context(0)
 d = ctx.scalars_generate(seed=20, n=n)
 ref = None
-K = 10
+K = 30
 for cfg, nl in [(c, nl) for c in cfgs for nl in lanes]:
     ctx.set_lanes(nl)
     b = ctx.bases_generate(seed=1000, n=n, g2=g2)
@@ -28,14 +29,21 @@ for cfg, nl in [(c, nl) for c in cfgs for nl in lanes]:
     r = ctx.msm(b, d)
     if ref is None:
         ref = r
+    depth = int(depth_env) if depth_env else nl
+    for _ in range(2):  # warm every lane
+        jobs = [ctx.msm_submit(b, d, n) for _ in range(nl)]
+        for j in jobs:
+            ctx.msm_wait(j)
     ctx.profile(True)
     ctx.profile_reset()
     t0 = time.time()
-    jobs = [ctx.msm_submit(b, d, n)]
-    for _ in range(K - 1):
-        jobs.append(ctx.msm_submit(b, d, n))
+    jobs = [ctx.msm_submit(b, d, n) for _ in range(depth)]
+    for _ in range(K - depth):
         ctx.msm_wait(jobs.pop(0))
-    r2 = ctx.msm_wait(jobs.pop(0))
+        jobs.append(ctx.msm_submit(b, d, n))
+    for j in jobs[:-1]:
+        ctx.msm_wait(j)
+    r2 = ctx.msm_wait(jobs[-1])
     dt = (time.time() - t0) / K
     ctx.profile(False)
     print(f"{cfg} lanes={nl}: 2^{log_n} {'G2' if g2 else 'G1'} pipelined {dt*1e3:.3f} ms -> {n/dt/1e6:.1f} Mpt/s "

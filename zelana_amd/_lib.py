@@ -85,6 +85,7 @@ SIGNATURES = [
     ("zkmi_pk_synthetic", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint32, sz, sz, ctypes.POINTER(vp)]),
     ("zkmi_groth16_setup", ctypes.c_int, [vp, vp, u64p, u64p, u64p, ctypes.POINTER(vp)]),
     ("zkmi_pk_serialize", ctypes.c_int, [vp, u8p, sz, ctypes.POINTER(sz)]),
+    ("zkmi_vk_canonical", ctypes.c_int, [vp, u8p, sz, u8p, sz, ctypes.POINTER(sz)]),
     ("zkmi_proof_to_solana_bytes", ctypes.c_int, [u64p, u64p, u64p, u8p]),
     ("zkmi_proof_serialize_compressed", ctypes.c_int, [u64p, u64p, u64p, u8p]),
 ]

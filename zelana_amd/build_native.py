@@ -16,6 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.environ.get("ZKMI_BUILD_DIR") or os.path.join(HERE, "build")
 LIB = os.environ.get("ZKMI_LIB_OUT") or os.path.join(HERE, "libzkmi.so")
+HOST = os.path.join(HERE, "host")
+HOST_LIB = os.path.join(HERE, "libzelana_prover.so")   # C++ mirror of the reference prover, above the C ABI
+HOST_TEST = os.path.join(HERE, "test_batch_prover")    # its C++ unit tests (tests/host/test_batch_prover.cpp)
+ROCM_LIB = "/opt/rocm/lib"
 ARCH = os.environ.get("ZKMI_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
@@ -64,9 +68,30 @@ def build(verbose: bool = False) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed: " + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+    _build_host(verbose)
     if verbose:
         print("built", LIB)
     return LIB
+
+
+def _build_host(verbose: bool):
+    """libzelana_prover.so (g++, links libzkmi.so) and its test binary."""
+    srcs = sorted(glob.glob(os.path.join(HOST, "*.cpp")))
+    hdrs = glob.glob(os.path.join(HOST, "*.h")) + [os.path.join(HERE, "..", "include", "zkmi.h")]
+    test_src = os.path.join(HERE, "..", "tests", "host", "test_batch_prover.cpp")
+    inc = ["-I" + HOST, "-I" + os.path.join(HERE, "..", "include")]
+    link = ["-L" + HERE, "-lzkmi", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath-link," + ROCM_LIB]
+    for out, cmd_srcs, kind in ((HOST_LIB, srcs, ["-shared", "-fPIC"]),
+                                (HOST_TEST, [s for s in srcs if not s.endswith("capi.cpp")] + [test_src], [])):
+        deps = cmd_srcs + hdrs + [LIB]
+        if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+            continue
+        cmd = ["g++", "-O2", "-std=c++17", "-Wall"] + kind + inc + ["-o", out] + cmd_srcs + link
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("host build failed: " + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+        if verbose:
+            print("built", out)
 
 
 if __name__ == "__main__":

@@ -982,6 +982,40 @@ int groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t tw[20], con
   return 0;
 }
 
+// VerifyingKey::deserialize_compressed (validated: on curve, G2 in the
+// subgroup; prover.rs:266-267) re-serialized: compute_vk_hash (:289-294)
+// hashes exactly these bytes.
+int vk_canonical(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, uint8_t* out, size_t cap, size_t* out_len) {
+  Rd r{bytes, len};
+  const uint8_t* alpha = r.take(32);
+  const uint8_t* g2s = r.take(3 * 64);
+  const uint64_t nabc = r.u64();
+  if (!r.ok || nabc == 0 || nabc > (1u << 24)) {
+    set_error("Failed to deserialize verifying key: truncated");
+    return ZKMI_EINVAL;
+  }
+  const uint8_t* abc = r.take(nabc * 32);
+  if (!r.ok || r.off != len) {
+    set_error("Failed to deserialize verifying key: %zu trailing / missing bytes", len - r.off);
+    return ZKMI_EINVAL;
+  }
+  std::vector<uint64_t> a1(8), g2(3 * 16), ic(nabc * 8);
+  ZK_TRY(decode_to_host(ctx, 0, alpha, 1, 1, a1.data()));
+  ZK_TRY(decode_to_host(ctx, 1, g2s, 3, 1, g2.data()));
+  ZK_TRY(decode_to_host(ctx, 0, abc, nabc, 1, ic.data()));
+  *out_len = len;
+  if (!out) return 0;
+  if (cap < len) {
+    set_error("vk_canonical: buffer too small");
+    return ZKMI_EINVAL;
+  }
+  g1_compress(a1.data(), out);
+  for (int i = 0; i < 3; i++) g2_compress(&g2[16 * i], out + 32 + 64 * i);
+  for (int i = 0; i < 8; i++) out[224 + i] = (uint8_t)(nabc >> (8 * i));
+  for (uint64_t i = 0; i < nabc; i++) g1_compress(&ic[8 * i], out + 232 + 32 * i);
+  return 0;
+}
+
 // ProvingKey::serialize_compressed (keygen.rs:103): vk | beta_g1 | delta_g1 |
 // a | b_g1 | b_g2 | h | l, each query a u64 length then points
 int pk_serialize(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {
@@ -1121,6 +1155,13 @@ int zkmi_groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t toxic[
     return ZKMI_EINVAL;
   }
   return groth16_setup(ctx, cs, toxic, g1, g2, out);
+}
+int zkmi_vk_canonical(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, uint8_t* out, size_t cap, size_t* out_len) {
+  if (!ctx || !bytes || !out_len) {
+    set_error("zkmi_vk_canonical: null argument");
+    return ZKMI_EINVAL;
+  }
+  return vk_canonical(ctx, bytes, len, out, cap, out_len);
 }
 int zkmi_pk_serialize(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {
   if (!pk || !len) {

@@ -284,6 +284,18 @@ class ProvingKey:
             pass
 
 
+def vk_canonical(ctx: Context, vk_bytes: bytes) -> bytes:
+    """VerifyingKey::deserialize_compressed (validated on the GPU) re-serialized."""
+    src = np.frombuffer(vk_bytes, np.uint8).copy()
+    ln = ctypes.c_size_t()
+    check(lib().zkmi_vk_canonical(ctx.h, src.ctypes.data_as(u8p), len(vk_bytes), None, 0, ctypes.byref(ln)),
+          "Failed to deserialize verifying key")
+    out = np.zeros(ln.value, np.uint8)
+    check(lib().zkmi_vk_canonical(ctx.h, src.ctypes.data_as(u8p), len(vk_bytes), out.ctypes.data_as(u8p), ln.value,
+                                  ctypes.byref(ln)), "Failed to deserialize verifying key")
+    return out.tobytes()
+
+
 def _limbs(x: int) -> np.ndarray:
     return np.array([(x >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], np.uint64)
 

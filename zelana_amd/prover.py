@@ -134,11 +134,13 @@ class Groth16Prover:
         cost ~15x the key) so every later prove runs one MSM window per query."""
         ctx = gpu.Context(device)
         pk = gpu.ProvingKey(ctx, pk_bytes, compressed)
-        if vk_bytes != pk.vk_bytes():
-            raise ValueError("Failed to deserialize verifying key: does not match the proving key's")
+        # as the reference: the VK is deserialized on its own (validated) and
+        # hashed in its canonical compressed form; it is not cross-checked
+        # against the proving key (prover.rs:263-277, 289-294)
+        vk = gpu.vk_canonical(ctx, vk_bytes)
         if precompute:
             pk.precompute()
-        return cls(ctx, pk, vk_bytes, circuit)
+        return cls(ctx, pk, vk, circuit)
 
     @classmethod
     def keygen(cls, device: int = 0, seed: int = 0, circuit_shape=None, precompute: bool = True):
