@@ -1,0 +1,150 @@
+"""Full-size parity (BASELINE.json configs[1-4] sizes) through properties that
+do not need the CPU oracle to redo the whole job:
+
+* NTT / INTT at 2^24 (configs[2]), plain and coset: round trip is the
+  identity; linearity NTT(a + b) = NTT(a) + NTT(b); and exact values at
+  sampled output indices for a sparse input, evaluated directly
+  (sum_j a_j omega^{jk}, omega = 5^((r-1)/2^28) ^ (2^28 / n), coset:
+  a_j -> a_j g^j) — the arkworks Radix2EvaluationDomain definition.
+* G1 MSM at 2^24 with the fixed-base table (configs[4]'s per-GPU scale at
+  N=4): linearity MSM(a) + MSM(b) = MSM(a + b); and a sparse-scalar MSM
+  equal to the oracle's sum over its non-zero terms.
+"""
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+
+pytestmark = pytest.mark.gpu
+R = O.R
+RL = np.array([R >> (64 * i) & 0xFFFFFFFFFFFFFFFF for i in range(4)], np.uint64)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from zelana_amd.gpu import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def add_mod_r(a, b):
+    """(n, 4) u64 canonical + (n, 4) -> mod r, vectorised with explicit carries."""
+    out = np.zeros_like(a)
+    carry = np.zeros(a.shape[0], np.uint64)
+    for i in range(4):
+        s = a[:, i] + b[:, i]
+        c1 = (s < a[:, i]).astype(np.uint64)
+        s2 = s + carry
+        c2 = (s2 < s).astype(np.uint64)
+        out[:, i] = s2
+        carry = c1 | c2
+    # subtract r where out >= r (sums < 2r < 2^255: no carry out of limb 3)
+    ge = np.ones(a.shape[0], bool)
+    decided = np.zeros(a.shape[0], bool)
+    for i in (3, 2, 1, 0):
+        gt = (out[:, i] > RL[i]) & ~decided
+        lt = (out[:, i] < RL[i]) & ~decided
+        ge[lt] = False
+        decided |= gt | lt
+    borrow = np.zeros(a.shape[0], np.uint64)
+    sub = out.copy()
+    for i in range(4):
+        d = sub[:, i] - RL[i]
+        b1 = (sub[:, i] < RL[i]).astype(np.uint64)
+        d2 = d - borrow
+        b2 = (d < borrow).astype(np.uint64)
+        sub[:, i] = d2
+        borrow = b1 | b2
+    out[ge] = sub[ge]
+    return out
+
+
+def to_int(row):
+    return sum(int(v) << (64 * i) for i, v in enumerate(row))
+
+
+def omega(log_n):
+    w = pow(5, (R - 1) >> 28, R)
+    return pow(w, 1 << (28 - log_n), R)
+
+
+@pytest.mark.parametrize("coset", [False, True])
+def test_ntt_2pow24_roundtrip_and_linearity(ctx, coset):
+    from zelana_amd.gpu import DeviceBuffer
+    log_n = 24
+    n = 1 << log_n
+    a = ctx.scalars_generate(seed=240 + coset, n=n)
+    b = ctx.scalars_generate(seed=250 + coset, n=n)
+    ha, hb = np.zeros((n, 4), np.uint64), np.zeros((n, 4), np.uint64)
+    a.download(ha)
+    b.download(hb)
+    hs = add_mod_r(ha, hb)
+    s = DeviceBuffer(ctx, n * 32)
+    s.upload(hs)
+    for buf in (a, b, s):
+        ctx.ntt_device(buf, log_n, False, coset)
+    fa, fb, fs = (np.zeros((n, 4), np.uint64) for _ in range(3))
+    a.download(fa)
+    b.download(fb)
+    s.download(fs)
+    assert np.array_equal(add_mod_r(fa, fb), fs)
+    assert not np.array_equal(fa, ha)
+    ctx.ntt_device(a, log_n, True, coset)
+    back = np.zeros((n, 4), np.uint64)
+    a.download(back)
+    assert np.array_equal(back, ha)
+
+
+@pytest.mark.parametrize("inverse,coset", [(False, False), (True, False), (False, True), (True, True)])
+def test_ntt_2pow24_sparse_exact(ctx, inverse, coset):
+    log_n = 24
+    n = 1 << log_n
+    rng = np.random.default_rng(24 + 2 * inverse + coset)
+    idx = rng.choice(n, 40, replace=False)
+    vals = [int.from_bytes(rng.bytes(32), "little") % R for _ in idx]
+    data = np.zeros((n, 4), np.uint64)
+    for j, v in zip(idx, vals):
+        data[j] = [(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)]
+    out = ctx.ntt(data, log_n, inverse, coset)
+    w = omega(log_n)
+    if inverse:
+        w = pow(w, R - 2, R)
+    ninv = pow(n, R - 2, R)
+    g = 5
+    for k in rng.choice(n, 12, replace=False):
+        acc = sum(v * pow(w, int(j) * int(k), R) for j, v in zip(idx, vals)) % R
+        if not inverse:
+            if coset:  # coset FFT: evaluations of a(g X)
+                acc = sum(v * pow(g, int(j), R) * pow(w, int(j) * int(k), R) for j, v in zip(idx, vals)) % R
+        else:
+            acc = acc * ninv % R
+            if coset:  # coset IFFT: coefficients scaled by g^-k
+                acc = acc * pow(pow(g, R - 2, R), int(k), R) % R
+        assert to_int(out[k]) == acc, (k, inverse, coset)
+
+
+def test_msm_2pow24_table_linearity_and_sparse(ctx):
+    from zelana_amd.gpu import DeviceBuffer, g1_add
+    n = 1 << 24
+    bases = ctx.bases_generate(seed=1024, n=n)
+    bases.precompute()
+    a = ctx.scalars_generate(seed=31, n=n)
+    b = ctx.scalars_generate(seed=32, n=n)
+    ha, hb = np.zeros((n, 4), np.uint64), np.zeros((n, 4), np.uint64)
+    a.download(ha)
+    b.download(hb)
+    s = DeviceBuffer(ctx, n * 32)
+    s.upload(add_mod_r(ha, hb))
+    ma, mb, ms = ctx.msm(bases, a), ctx.msm(bases, b), ctx.msm(bases, s)
+    assert np.array_equal(g1_add(ma, mb), ms)
+    # sparse scalars: the full 2^24 run against the oracle over its non-zero terms
+    rng = np.random.default_rng(7)
+    idx = np.sort(rng.choice(n, 300, replace=False))
+    sp = np.zeros((n, 4), np.uint64)
+    sp[idx] = ha[idx]
+    d = DeviceBuffer(ctx, n * 32)
+    d.upload(sp)
+    got = ctx.msm(bases, d)
+    pts = bases.export()[idx]
+    assert np.array_equal(got, O.msm_g1(np.ascontiguousarray(pts), np.ascontiguousarray(ha[idx])))
