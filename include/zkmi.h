@@ -172,8 +172,12 @@ int zkmi_pk_info(const zkmi_pk* pk, uint64_t out[3]);
 /* arkworks-compressed VerifyingKey bytes embedded in the pk (for vk hash) */
 /* Fixed-base tables for all five queries (zkmi_bases_precompute, window
  * picked per query length; factor 0 = full).  Proofs are unchanged; a full
- * table costs ~15x the key's HBM footprint (2^22 domain: ~24 GB). */
+ * table costs ~15x the key's HBM footprint (2^22 domain: ~24 GB).  When at
+ * least 1/8 of the variables have both B bases at infinity (B_i(t) = 0: no B
+ * row reads them), the B-query MSMs are first compacted to the others. */
 int zkmi_pk_precompute(zkmi_pk* pk, int factor);
+/* number of variables the B-query MSMs run over (V - 1 when not compacted) */
+int zkmi_pk_b_terms(const zkmi_pk* pk, uint64_t* out);
 int zkmi_pk_vk_bytes(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len);
 
 /* Full proof.  z: full assignment (One, instance..., witness...), canonical.

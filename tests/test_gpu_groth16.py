@@ -112,8 +112,15 @@ def test_synthetic_prove_and_witness_map(ctx, m, l, w, sat):
     want = _oracle_prove(opk, st, z, r, s)
     for g, wv in zip(got, want):
         assert np.array_equal(g, wv)
-    # fixed-base tables on every query (full for small keys, partial otherwise)
+    # fixed-base tables on every query (full for small keys, partial otherwise);
+    # satisfied systems read only the free variables in B, so the B MSMs are
+    # compacted to those (product witnesses have B bases at infinity)
     pk.precompute(0 if m < 2500 else 3)
+    nv = l + w
+    if sat:
+        assert pk.b_terms() <= nv - m
+    else:
+        assert pk.b_terms() == nv - 1
     for g, wv in zip(gpu.groth16_prove(ctx, pk, cs, z, r, s), want):
         assert np.array_equal(g, wv)
     n = 1

@@ -77,6 +77,7 @@ SIGNATURES = [
     ("zkmi_pk_destroy", None, [vp]),
     ("zkmi_pk_info", ctypes.c_int, [vp, u64p]),
     ("zkmi_pk_precompute", ctypes.c_int, [vp, ctypes.c_int]),
+    ("zkmi_pk_b_terms", ctypes.c_int, [vp, u64p]),
     ("zkmi_pk_vk_bytes", ctypes.c_int, [vp, u8p, sz, ctypes.POINTER(sz)]),
     ("zkmi_groth16_prove", ctypes.c_int, [vp, vp, ctypes.POINTER(R1CSStruct), u64p, u64p, u64p, u64p, u64p, u64p]),
     ("zkmi_r1cs_create", ctypes.c_int, [vp, ctypes.POINTER(R1CSStruct), ctypes.POINTER(vp)]),

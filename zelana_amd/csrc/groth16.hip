@@ -30,6 +30,13 @@ struct zkmi_pk {
   uint64_t a0[8], b1_0[8], b2_0[16];
   zkmi_bases *a_query = nullptr, *b_g1_query = nullptr, *b_g2_query = nullptr, *h_query_rev = nullptr,
              *l_query = nullptr;
+  // B queries without their points at infinity (zkmi_pk_precompute): B_i(t) =
+  // 0 for every variable no B row reads, half of them in a MiMC circuit.  The
+  // prove MSMs run over b_idx's variables only (same sums: an infinity base
+  // adds nothing).  The full sets stay for serialization.
+  zkmi_bases *b_g1_c = nullptr, *b_g2_c = nullptr;
+  uint32_t* d_bidx = nullptr;  // kept variable indices, ascending, in [1, V)
+  size_t nb_c = 0;
   std::vector<uint8_t> vk_compressed;
 };
 
@@ -669,6 +676,105 @@ int pk_load(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, int compressed, zkm
   return 0;
 }
 
+// ------------------------------------------------------------ B-query compaction
+__global__ void __launch_bounds__(256) k_gather_scalars(const uint32_t* __restrict__ z, const uint32_t* __restrict__ idx,
+                                                        size_t n, uint32_t* __restrict__ out) {
+  size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const uint4* s = reinterpret_cast<const uint4*>(z + (size_t)idx[k] * 8);
+  uint4* d = reinterpret_cast<uint4*>(out + k * 8);
+  d[0] = s[0];
+  d[1] = s[1];
+}
+template <int PW>  // words per point
+__global__ void __launch_bounds__(256) k_gather_points(const uint32_t* __restrict__ pts,
+                                                       const uint32_t* __restrict__ idx, size_t n,
+                                                       uint32_t* __restrict__ out) {
+  size_t k = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n) return;
+  const uint4* s = reinterpret_cast<const uint4*>(pts + (size_t)idx[k] * PW);
+  uint4* d = reinterpret_cast<uint4*>(out + k * PW);
+#pragma unroll
+  for (int i = 0; i < PW / 4; i++) d[i] = s[i];
+}
+// live[i] = 1 unless both B bases of variable i are at infinity (bit 31 of a
+// point's last word)
+__global__ void __launch_bounds__(256) k_b_live(const uint32_t* __restrict__ b1, const uint32_t* __restrict__ b2,
+                                                size_t n, uint8_t* __restrict__ live) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  live[i] = !((b1[i * 16 + 15] >> 31) & (b2[i * 32 + 31] >> 31));
+}
+
+static int gather_bases(zkmi_ctx* ctx, const zkmi_bases* src, const uint32_t* d_idx, size_t n, zkmi_bases** out) {
+  const int pw = src->g2 ? 32 : 16;
+  uint32_t* d_pts = nullptr;
+  if (hipMalloc(&d_pts, std::max<size_t>(1, n) * pw * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("hipMalloc(%zu) failed for compacted bases", n * pw * 4);
+    return ZKMI_ENOMEM;
+  }
+  unsigned grid = (unsigned)((n + 255) / 256);
+  if (src->g2) k_gather_points<32><<<grid, 256, 0, ctx->stream>>>(src->d_pts, d_idx, n, d_pts);
+  else k_gather_points<16><<<grid, 256, 0, ctx->stream>>>(src->d_pts, d_idx, n, d_pts);
+  if (hipGetLastError() != hipSuccess) {
+    hipFree(d_pts);
+    set_error("gather_bases: launch failed");
+    return ZKMI_EHIP;
+  }
+  zkmi_bases* b = new zkmi_bases;
+  b->ctx = ctx;
+  b->g2 = src->g2;
+  b->n = n;
+  b->d_pts = d_pts;
+  *out = b;
+  return 0;
+}
+
+// Drop the B variables whose bases are both at infinity when that removes at
+// least 1/8 of them (a no-op for dense keys).  One-time, at precompute.
+int pk_compact_b(zkmi_pk* pk) {
+  zkmi_ctx* ctx = pk->ctx;
+  const size_t nv = pk->num_instance + pk->num_witness;
+  if (nv < 2 || pk->b_g1_query->n < nv || pk->b_g2_query->n < nv) return 0;
+  const size_t m = nv - 1;  // variables 1..V-1 (the One term is added outside the MSM)
+  uint8_t* d_live;
+  ZK_TRY(ctx->ws.get("g16_blive", m, (void**)&d_live));
+  k_b_live<<<(unsigned)((m + 255) / 256), 256, 0, ctx->stream>>>(pk->b_g1_query->d_pts + 16, pk->b_g2_query->d_pts + 32,
+                                                                 m, d_live);
+  ZK_HIP(hipGetLastError());
+  std::vector<uint8_t> live(m);
+  ZK_HIP(hipMemcpyAsync(live.data(), d_live, m, hipMemcpyDeviceToHost, ctx->stream));
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  std::vector<uint32_t> idx;
+  idx.reserve(m);
+  for (size_t i = 0; i < m; i++)
+    if (live[i]) idx.push_back((uint32_t)(i + 1));
+  if (idx.empty() || idx.size() > m - m / 8) return 0;
+  uint32_t* d_idx = nullptr;
+  if (hipMalloc(&d_idx, idx.size() * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("hipMalloc failed for the B index list");
+    return ZKMI_ENOMEM;
+  }
+  int rc = hipMemcpy(d_idx, idx.data(), idx.size() * 4, hipMemcpyHostToDevice) == hipSuccess ? 0 : ZKMI_EHIP;
+  zkmi_bases *b1 = nullptr, *b2 = nullptr;
+  if (!rc) rc = gather_bases(ctx, pk->b_g1_query, d_idx, idx.size(), &b1);
+  if (!rc) rc = gather_bases(ctx, pk->b_g2_query, d_idx, idx.size(), &b2);
+  if (!rc) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : ZKMI_EHIP;
+  if (rc) {
+    zkmi_bases_destroy(b1);
+    zkmi_bases_destroy(b2);
+    hipFree(d_idx);
+    return rc;
+  }
+  pk->b_g1_c = b1;
+  pk->b_g2_c = b2;
+  pk->d_bidx = d_idx;
+  pk->nb_c = idx.size();
+  return 0;
+}
+
 // ------------------------------------------------------------ prove
 // core: R1CS and full assignment z already resident in HBM
 int groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
@@ -694,7 +800,17 @@ int groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, 
   uint64_t h_acc[8], l_acc[8], a_acc[8], b1_acc[8], b2_acc[16];
   int rc = 0;
   rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
-  if (!rc) {
+  if (!rc && pk->d_bidx) {  // a over z[1..V]; b1 / b2 over the compacted B variables
+    uint32_t* zb;
+    rc = ctx->ws.get("g16_zb", pk->nb_c * 32, (void**)&zb);
+    if (!rc) {
+      k_gather_scalars<<<(unsigned)((pk->nb_c + 255) / 256), 256, 0, ctx->stream>>>(dz, pk->d_bidx, pk->nb_c, zb);
+      rc = hipGetLastError() == hipSuccess ? 0 : ZKMI_EHIP;
+    }
+    if (!rc) rc = msm_submit(ctx, pk->a_query, 1, dz + 8, nv - 1, &jobs[2]);
+    const zkmi_bases* bq[2] = {pk->b_g1_c, pk->b_g2_c};
+    if (!rc) rc = msm_submit_shared(ctx, bq, 2, 0, zb, pk->nb_c, &jobs[3]);
+  } else if (!rc) {
     const zkmi_bases* abq[3] = {pk->a_query, pk->b_g1_query, pk->b_g2_query};
     rc = msm_submit_shared(ctx, abq, 3, 1, dz + 8, nv - 1, &jobs[2]);
   }
@@ -1078,6 +1194,9 @@ void zkmi_pk_destroy(zkmi_pk* pk) {
   zkmi_bases_destroy(pk->a_query);
   zkmi_bases_destroy(pk->b_g1_query);
   zkmi_bases_destroy(pk->b_g2_query);
+  zkmi_bases_destroy(pk->b_g1_c);
+  zkmi_bases_destroy(pk->b_g2_c);
+  if (pk->d_bidx) hipFree(pk->d_bidx);
   zkmi_bases_destroy(pk->h_query_rev);
   zkmi_bases_destroy(pk->l_query);
   delete pk;
@@ -1093,12 +1212,26 @@ int zkmi_pk_precompute(zkmi_pk* pk, int factor) {
     zk::set_error("zkmi_pk_precompute: null key");
     return ZKMI_EINVAL;
   }
-  zkmi_bases* qs[5] = {pk->h_query_rev, pk->l_query, pk->a_query, pk->b_g1_query, pk->b_g2_query};
+  if (!pk->d_bidx && !pk->b_g1_query->tc) {
+    int rc = zk::pk_compact_b(pk);
+    if (rc) return rc;
+  }
+  const bool compact = pk->d_bidx != nullptr;
+  zkmi_bases* qs[5] = {pk->h_query_rev, pk->l_query, pk->a_query, compact ? pk->b_g1_c : pk->b_g1_query,
+                       compact ? pk->b_g2_c : pk->b_g2_query};
   for (zkmi_bases* b : qs) {
     if (!b || b->tc) continue;
     int rc = zk::bases_precompute(b, zk::table_window(b->n), factor);
     if (rc) return rc;
   }
+  return 0;
+}
+int zkmi_pk_b_terms(const zkmi_pk* pk, uint64_t* out) {
+  if (!pk || !out) {
+    zk::set_error("zkmi_pk_b_terms: null argument");
+    return ZKMI_EINVAL;
+  }
+  *out = pk->d_bidx ? pk->nb_c : pk->num_instance + pk->num_witness - 1;
   return 0;
 }
 int zkmi_pk_vk_bytes(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {

@@ -963,8 +963,11 @@ __global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ x
 __device__ __forceinline__ uint32_t insert_bit(uint32_t t, int bit) {
   return (((t >> bit) << (bit + 1)) | (1u << bit) | (t & ((1u << bit) - 1)));
 }
+#ifndef ZK_BR_WPE
+#define ZK_BR_WPE 4
+#endif
 template <class G, bool BITS>
-__global__ void __launch_bounds__(256) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
                                                 const uint32_t* __restrict__ bstart, int lb, int hb, int W, int sr,
                                                 int sc, int sb, uint32_t* __restrict__ out0,
                                                 uint32_t* __restrict__ out1) {
@@ -1065,6 +1068,74 @@ __global__ void __launch_bounds__(256) k_msm_br(const uint32_t* __restrict__ src
     }
     st_xyzz<G>(dst, v);
   }
+}
+
+// Rows / columns in strips (replaces the FUSED pass of k_msm_br when a row or
+// column fits one wave): one wave per row h (C[w][h] = sum_l B[w][h, l]) or
+// column l (D[w][l] = sum_h B[w][h, l]); lane t folds the contiguous strip
+// [t L, (t + 1) L) of its line sequentially, then one 6-level LDS tree.  For
+// 2^19-bucket windows this issues ~40% fewer lane-additions than 256-bucket
+// jobs (4 folds + 6 levels each), and the bucket reduction runs beside the
+// other lane's accumulation, where wasted VALU issue is what it costs.
+template <class G>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br_strip(const uint32_t* __restrict__ buckets,
+                                                      const uint32_t* __restrict__ bstart, int lb, int hb, int W,
+                                                      int sr, int sc, uint32_t* __restrict__ outC,
+                                                      uint32_t* __restrict__ outD) {
+  using F = typename G::F;
+  constexpr int XW = 4 * G::CW;
+  __shared__ Xyzz<F> sh[4][32];
+  const int bb = lb + hb;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t job = blockIdx.x * 4 + wave;
+  const uint32_t nrow = ((uint32_t)W << hb) * sr, ncol = ((uint32_t)W << lb) * sc;
+  const bool live = job < nrow + ncol;
+  uint32_t len = 0, stride = 1, bucket0 = 0;
+  uint32_t* dst = nullptr;
+  if (live) {
+    if (job < nrow) {  // segment g of row h of window w (C[h][g], as k_msm_br)
+      const uint32_t rh = job / sr, g = job % sr, w = rh >> hb, h = rh & ((1u << hb) - 1);
+      len = (1u << lb) / sr;
+      bucket0 = (w << bb) + (h << lb) + g * len;
+      stride = 1;
+      dst = outC + (size_t)job * XW;
+    } else {  // segment g of column l of window w
+      const uint32_t jj = job - nrow, cl = jj / sc, g = jj % sc, w = cl >> lb, l = cl & ((1u << lb) - 1);
+      len = (1u << hb) / sc;
+      bucket0 = (w << bb) + ((g * len) << lb) + l;
+      stride = 1u << lb;
+      dst = outD + (size_t)jj * XW;
+    }
+  }
+  const uint32_t L = (len + 63) >> 6;  // strip per lane
+  const uint32_t Lr = (((1u << lb) / sr) + 63) >> 6, Lc = (((1u << hb) / sc) + 63) >> 6;
+  const uint32_t Lmax = Lr > Lc ? Lr : Lc;  // block-uniform loop bound
+  Xyzz<F> v = xyzz_inf<F>();
+  for (uint32_t step = 0; step < Lmax + 6; step++) {
+    Xyzz<F> q;
+    bool act = false;
+    if (step < Lmax) {
+      const uint32_t t = lane * L + step;
+      if (live && step < L && t < len) {
+        const uint32_t b = bucket0 + t * stride;
+        if (bstart[b + 1] > bstart[b]) {
+          q = ld_xyzz<G>(buckets + (size_t)b * XW);
+          act = true;
+        }
+      }
+    } else {
+      const uint32_t sz = 32u >> (step - Lmax);
+      if (lane >= sz && lane < 2 * sz) sh[wave][lane - sz] = v;
+      __syncthreads();
+      if (lane < sz) {
+        q = sh[wave][lane];
+        act = !xyzz_is_inf(q);
+      }
+    }
+    if (act) v = xyzz_is_inf(v) ? q : xyzz_add(v, q);
+    if (step >= Lmax) __syncthreads();
+  }
+  if (live && lane == 0) st_xyzz<G>(dst, v);
 }
 
 // ------------------------------------------------------------ base upload
@@ -1810,7 +1881,16 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   }
   // bucket reduction -> W*(bb+1) canonical bit sums
   uint32_t *Cb, *Db, *sums;
-  const int sr = lb > 8 ? 1 << (lb - 8) : 1, sc = hb > 8 ? 1 << (hb - 8) : 1;  // <= 256 buckets per wave job
+  // G1 windows with rows / columns of >= 2^9 buckets: strip-folding waves of
+  // 512 contiguous buckets (8 per lane; 2^20 table MSM: 0.34 -> 0.28 ms
+  // isolated); otherwise <= 256-bucket strided wave jobs (G2 keeps those).
+  static const int strip_fold = [] {  // buckets folded per lane before the tree
+    const char* e = getenv("ZKMI_BR_STRIP");
+    return e ? atoi(e) : 8;
+  }();
+  const bool strip = strip_fold > 0 && G::CW == 8 && hb >= 9;
+  const int segb = strip ? 64 * strip_fold : 256;  // buckets per wave job
+  const int sr = (1 << lb) > segb ? (1 << lb) / segb : 1, sc = (1 << hb) > segb ? (1 << hb) / segb : 1;
   // bit-sum segments: the longest bit job sums max(2^hb * sr, 2^(lb-1) * sc) terms
   const uint32_t maxterms = std::max((1u << hb) * sr, (1u << (lb - 1)) * sc);
   const int sb = (int)((maxterms + 255) / 256);
@@ -1819,8 +1899,14 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   ZK_TRY(ws.get("msm_sums", (size_t)W * (bb + 1) * sb * XW * 4, (void**)&sums));
   {
     ScopedKernelTimer tm(ctx, "msm_bucket_reduce", st);
-    uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc)), jobs2 = (uint32_t)W * (bb + 1) * sb;
-    k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, st>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, Cb, Db);
+    uint32_t jobs2 = (uint32_t)W * (bb + 1) * sb;
+    if (strip) {  // one wave per row / column
+      uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc));
+      k_msm_br_strip<G><<<(jobs1 + 3) / 4, 256, 0, st>>>(buckets, bstart, lb, hb, W, sr, sc, Cb, Db);
+    } else {
+      uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc));
+      k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, st>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, Cb, Db);
+    }
     k_msm_br<G, true><<<(jobs2 + 3) / 4, 256, 0, st>>>(Cb, Db, nullptr, lb, hb, W, sr, sc, sb, sums, nullptr);
     ZK_HIP(hipGetLastError());
   }

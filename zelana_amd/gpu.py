@@ -238,6 +238,13 @@ class ProvingKey:
         check(lib().zkmi_pk_precompute(self.h, factor), "zkmi_pk_precompute")
         return self
 
+    def b_terms(self) -> int:
+        """Variables the B-query MSMs run over (fewer than V - 1 once
+        precompute() has dropped the ones whose B bases are at infinity)."""
+        v = np.zeros(1, np.uint64)
+        check(lib().zkmi_pk_b_terms(self.h, _p64(v)), "zkmi_pk_b_terms")
+        return int(v[0])
+
     def vk_bytes(self) -> bytes:
         ln = ctypes.c_size_t()
         check(lib().zkmi_pk_vk_bytes(self.h, None, 0, ctypes.byref(ln)))
