@@ -936,15 +936,27 @@ __global__ void __launch_bounds__(256) k_setup_lagrange(const uint32_t* __restri
   st_fe(u + i * 8, reduce<FrP>(mul<FrP>(mul<FrP>(ld_fe(sc + 8 * SC_ZTN), w), inv)));
 }
 // column sums over a CSC matrix: out_j = sum_k val_k u_{row_k} (+ u_{m+j} for
-// j < l in A), canonical value form
-__global__ void __launch_bounds__(256) k_setup_cols(const uint64_t* __restrict__ colptr,
+// j < l in A), canonical value form.  Columns are cut into segments of at most
+// SETUP_SEG entries (one thread each) so that a dense column (the One
+// variable: every row of a constant-heavy circuit) does not serialise the
+// launch; a second pass adds each column's segment partials.
+#define SETUP_SEG 256
+__global__ void __launch_bounds__(256) k_setup_segs(const uint64_t* __restrict__ segk, size_t nseg,
                                                     const uint32_t* __restrict__ row, const uint32_t* __restrict__ val,
-                                                    const uint32_t* __restrict__ u, size_t m, size_t l, size_t nv,
-                                                    int is_a, uint32_t* __restrict__ out) {
+                                                    const uint32_t* __restrict__ u, uint32_t* __restrict__ part) {
+  const size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (s >= nseg) return;
+  Fe acc = fe_zero();
+  for (uint64_t k = segk[s]; k < segk[s + 1]; k++) acc = add<FrP>(acc, mul<FrP>(ld_fe(val + k * 8), ld_fe(u + (size_t)row[k] * 8)));
+  st_fe(part + s * 8, acc);  // [0, 2p): fits 256 bits
+}
+__global__ void __launch_bounds__(256) k_setup_cols(const uint64_t* __restrict__ colseg,
+                                                    const uint32_t* __restrict__ part, const uint32_t* __restrict__ u,
+                                                    size_t m, size_t l, size_t nv, int is_a, uint32_t* __restrict__ out) {
   const size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (j >= nv) return;
   Fe acc = fe_zero();
-  for (uint64_t k = colptr[j]; k < colptr[j + 1]; k++) acc = add<FrP>(acc, mul<FrP>(ld_fe(val + k * 8), ld_fe(u + (size_t)row[k] * 8)));
+  for (uint64_t s = colseg[j]; s < colseg[j + 1]; s++) acc = add<FrP>(acc, ld_fe(part + s * 8));
   if (is_a && j < l) acc = add<FrP>(acc, mul<FrP>(ld_fe(u + (m + j) * 8), Fe{{1, 0, 0, 0, 0, 0, 0, 0, 0}}));
   st_fe(out + j * 8, reduce<FrP>(acc));
 }
@@ -1027,15 +1039,30 @@ int groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t tw[20], con
     std::vector<uint64_t> cp, cv;
     std::vector<uint32_t> rows;
     csr_to_csc(rps[t], cols[t], vals[t], m, nv, cp, rows, cv);
-    uint64_t* d_cp;
-    uint32_t *d_rows, *d_val;
-    ZK_TRY(ctx->ws.get("setup_cp", cp.size() * 8, (void**)&d_cp));
+    // segments: column j owns [colseg[j], colseg[j + 1]), segment s covers
+    // entries [segk[s], segk[s + 1])
+    std::vector<uint64_t> colseg(nv + 1), segk;
+    segk.reserve(cp[nv] / SETUP_SEG + nv + 1);
+    for (size_t j = 0; j < nv; j++) {
+      colseg[j] = segk.size();
+      for (uint64_t k = cp[j]; k < cp[j + 1]; k += SETUP_SEG) segk.push_back(k);
+    }
+    colseg[nv] = segk.size();
+    const size_t nseg = segk.size();
+    segk.push_back(cp[nv]);
+    uint64_t *d_colseg, *d_segk;
+    uint32_t *d_rows, *d_val, *d_part;
+    ZK_TRY(ctx->ws.get("setup_colseg", colseg.size() * 8, (void**)&d_colseg));
+    ZK_TRY(ctx->ws.get("setup_segk", segk.size() * 8, (void**)&d_segk));
+    ZK_TRY(ctx->ws.get("setup_part", std::max<size_t>(1, nseg) * 32, (void**)&d_part));
     ZK_TRY(ctx->ws.get("setup_rows", rows.size() * 4, (void**)&d_rows));
     ZK_TRY(ctx->ws.get("setup_cval", cv.size() * 8, (void**)&d_val));
-    ZK_HIP(hipMemcpyAsync(d_cp, cp.data(), cp.size() * 8, hipMemcpyHostToDevice, st));
+    ZK_HIP(hipMemcpyAsync(d_colseg, colseg.data(), colseg.size() * 8, hipMemcpyHostToDevice, st));
+    ZK_HIP(hipMemcpyAsync(d_segk, segk.data(), segk.size() * 8, hipMemcpyHostToDevice, st));
     ZK_HIP(hipMemcpyAsync(d_rows, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, st));
     ZK_HIP(hipMemcpyAsync(d_val, cv.data(), cv.size() * 8, hipMemcpyHostToDevice, st));
-    k_setup_cols<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(d_cp, d_rows, d_val, u, m, l, nv, t == 0, outs[t]);
+    if (nseg) k_setup_segs<<<(unsigned)((nseg + 255) / 256), 256, 0, st>>>(d_segk, nseg, d_rows, d_val, u, d_part);
+    k_setup_cols<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(d_colseg, d_part, u, m, l, nv, t == 0, outs[t]);
     ZK_HIP(hipStreamSynchronize(st));  // host vectors die with this iteration
   }
   k_setup_lscalars<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(va, vb, vc, d_sc, l, nv, abc + 3 * 8, lsc);
@@ -1221,7 +1248,7 @@ int zkmi_pk_precompute(zkmi_pk* pk, int factor) {
                        compact ? pk->b_g2_c : pk->b_g2_query};
   for (zkmi_bases* b : qs) {
     if (!b || b->tc) continue;
-    int rc = zk::bases_precompute(b, zk::table_window(b->n), factor);
+    int rc = zk::bases_precompute(b, zk::table_window(b->n, b->g2), factor);
     if (rc) return rc;
   }
   return 0;

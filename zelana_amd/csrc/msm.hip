@@ -1585,12 +1585,16 @@ int bases_precompute(zkmi_bases* b, int c, int factor) {
 // Window for a full table over N bases: one window of W(c)*N entries and 2^(c-1)
 // buckets; bucket reduction costs ~2.5 additions per bucket.  From 2^18
 // buckets on, the accumulation runs one lane per bucket (k_acc_items).
-int table_window(size_t N) {
+int table_window(size_t N, int g2) {
   static const int env_c = [] {
     const char* e = getenv("ZKMI_TABLE_C");  // experiments: pin the table window
     return e ? atoi(e) : 0;
   }();
   if (env_c >= 4 && env_c <= 22) return env_c;
+  // (G2: c = 17 below 2^21 points is faster for a lone MSM, 2^19: 4.45 ->
+  // 3.50 ms, but in a prove it splits B1 / B2's shared sort: zelana_batch 66
+  // -> 61 proofs/s.  Same window for both groups.)
+  (void)g2;
   int best = 8;
   double cost = 1e300;
   for (int c = 6; c <= 20; c++) {
@@ -1881,15 +1885,20 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   }
   // bucket reduction -> W*(bb+1) canonical bit sums
   uint32_t *Cb, *Db, *sums;
-  // G1 windows with rows / columns of >= 2^9 buckets: strip-folding waves of
-  // 512 contiguous buckets (8 per lane; 2^20 table MSM: 0.34 -> 0.28 ms
-  // isolated); otherwise <= 256-bucket strided wave jobs (G2 keeps those).
+  // Windows with rows / columns of >= 2^9 buckets: strip-folding waves of
+  // contiguous buckets (G1: 8 per lane, 2^20 table MSM 0.34 -> 0.28 ms
+  // isolated; G2: 16); otherwise <= 256-bucket strided wave jobs.
   static const int strip_fold = [] {  // buckets folded per lane before the tree
     const char* e = getenv("ZKMI_BR_STRIP");
     return e ? atoi(e) : 8;
   }();
-  const bool strip = strip_fold > 0 && G::CW == 8 && hb >= 9;
-  const int segb = strip ? 64 * strip_fold : 256;  // buckets per wave job
+  static const int strip_fold2 = [] {  // G2: 16 per lane (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
+    const char* e = getenv("ZKMI_BR_STRIP_G2");
+    return e ? atoi(e) : 16;
+  }();
+  const int fold = G::CW == 8 ? strip_fold : strip_fold2;
+  const bool strip = fold > 0 && hb >= 9;
+  const int segb = strip ? 64 * fold : 256;  // buckets per wave job
   const int sr = (1 << lb) > segb ? (1 << lb) / segb : 1, sc = (1 << hb) > segb ? (1 << hb) / segb : 1;
   // bit-sum segments: the longest bit job sums max(2^hb * sr, 2^(lb-1) * sc) terms
   const uint32_t maxterms = std::max((1u << hb) * sr, (1u << (lb - 1)) * sc);

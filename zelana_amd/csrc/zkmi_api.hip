@@ -251,7 +251,7 @@ int zkmi_bases_precompute(zkmi_bases* b, int c, int factor) {
     set_error("zkmi_bases_precompute: base set already has a table (window %d)", b->tc);
     return ZKMI_EINVAL;
   }
-  return bases_precompute(b, c > 0 ? c : table_window(b->n), factor);
+  return bases_precompute(b, c > 0 ? c : table_window(b->n, b->g2), factor);
 }
 int zkmi_bases_info(const zkmi_bases* b, uint64_t out[4]) {
   if (!b) {

@@ -132,7 +132,7 @@ int bases_export(const zkmi_bases* b, uint64_t* host_out);
 // d_out[i] = d_scalars[i] * gen: canonical scalars (8 x u32) -> canonical affine
 int fixed_base_mul(zkmi_ctx* ctx, int g2, const uint64_t* gen, const uint32_t* d_scalars, size_t n, uint32_t* d_out);
 int bases_precompute(zkmi_bases* b, int c, int factor);
-int table_window(size_t N);
+int table_window(size_t N, int g2 = 0);
 int scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, void* d_out);
 
 // NTT entry (ntt.hip): in-place on device, natural order
