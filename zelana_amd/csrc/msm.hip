@@ -163,11 +163,28 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__
 // addition is exact), so neither pass needs to be stable.
 constexpr int RS_THREADS = 256;
 
+// e / ne without a 64-bit integer division (~100 VALU instructions): a
+// double-precision estimate (off by at most one for e < 2^52) and a fix-up.
+__device__ __forceinline__ void rs_divmod(uint64_t e, uint32_t ne, double inv_ne, uint32_t& w, uint32_t& i) {
+  uint64_t q = (uint64_t)((double)e * inv_ne);
+  int64_t r = (int64_t)(e - q * ne);
+  if (r < 0) {
+    q--;
+    r += ne;
+  } else if (r >= (int64_t)ne) {
+    q++;
+    r -= ne;
+  }
+  w = (uint32_t)q;
+  i = (uint32_t)r;
+}
+
 __device__ __forceinline__ bool rs_key(const int32_t* __restrict__ digits, uint64_t e, uint32_t ne, uint32_t B,
                                        uint32_t& key, uint32_t& val) {
   int32_t d = digits[e];
   if (d == 0) return false;
-  uint32_t w = (uint32_t)(e / ne), i = (uint32_t)(e - (uint64_t)w * ne);
+  uint32_t w, i;
+  rs_divmod(e, ne, 1.0 / (double)ne, w, i);
   key = w * B + (uint32_t)(d < 0 ? -d : d) - 1;
   val = i | (d < 0 ? 0x80000000u : 0u);
   return true;
@@ -180,13 +197,57 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_count(const int32_t* __res
   for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) hist[x] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * C1;
-  for (uint32_t k = threadIdx.x; k < C1; k += RS_THREADS) {
-    uint64_t e = base + k;
-    uint32_t key, val;
-    if (e < M && rs_key(digits, e, ne, B, key, val)) atomicAdd(&hist[key >> lob], 1u);
+  const double inv_ne = 1.0 / (double)ne;
+  constexpr int U = 8;  // loads in flight per thread
+  for (uint32_t k0 = 0; k0 < C1; k0 += U * RS_THREADS) {
+    int32_t d[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t e = base + k0 + u * RS_THREADS + threadIdx.x;
+      d[u] = (k0 + u * RS_THREADS + threadIdx.x < C1 && e < M) ? digits[e] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (d[u] == 0) continue;
+      uint32_t w, i;
+      rs_divmod(base + k0 + u * RS_THREADS + threadIdx.x, ne, inv_ne, w, i);
+      atomicAdd(&hist[(w * B + (uint32_t)(d[u] < 0 ? -d[u] : d[u]) - 1) >> lob], 1u);
+    }
   }
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) cnt1[(size_t)x * nc1 + blockIdx.x] = hist[x];
+}
+
+
+// Exclusive scan of the bin counts hist[0..nb) into lstart, in a
+// thread-strided bin order: thread t owns bins t, t + 256, ...  Any bin order
+// works (each bin's entries only need to be contiguous in the LDS tile), and
+// this one keeps the LDS accesses conflict-free.  Wave scans by shuffles, one
+// barrier to combine the 4 waves.  tmp has RS_THREADS / 64 words.
+__device__ __forceinline__ uint32_t rs_block_scan(const uint32_t* hist, uint32_t* lstart, uint32_t nb, uint32_t* tmp) {
+  uint32_t sum = 0;
+  for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) sum += hist[x];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= (unsigned)off) inc += t;
+  }
+  if (lane == 63) tmp[wid] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum, total = 0;
+#pragma unroll
+  for (int w = 0; w < RS_THREADS / 64; w++) {
+    const uint32_t tw = tmp[w];
+    if ((uint32_t)w < wid) run += tw;
+    total += tw;
+  }
+  for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) {
+    lstart[x] = run;
+    run += hist[x];
+  }
+  return total;
 }
 
 // Scatter through LDS: each sub-tile of RS_ST entries is first ordered by bin
@@ -194,37 +255,9 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_count(const int32_t* __res
 // that consecutive lanes store consecutive addresses of one bin's run.
 // Without this the stores of a wave hit 64 different lines and partially
 // written lines get evicted (measured: ~10x slower than the reads).
-constexpr int RS_ST = 4096;
-constexpr int RS_PER = RS_ST / RS_THREADS;
-
-// exclusive block scan of a[0..nb) in place (nb <= 8192); returns nothing,
-// tmp has RS_THREADS words
-__device__ __forceinline__ void rs_block_scan(uint32_t* a, uint32_t nb, uint32_t* tmp) {
-  const uint32_t per = (nb + RS_THREADS - 1) / RS_THREADS, b0 = threadIdx.x * per;
-  uint32_t sum = 0;
-  for (uint32_t k = 0; k < per; k++)
-    if (b0 + k < nb) sum += a[b0 + k];
-  tmp[threadIdx.x] = sum;
-  __syncthreads();
-  for (int off = 1; off < RS_THREADS; off <<= 1) {
-    uint32_t t = threadIdx.x >= (unsigned)off ? tmp[threadIdx.x - off] : 0;
-    __syncthreads();
-    tmp[threadIdx.x] += t;
-    __syncthreads();
-  }
-  uint32_t run = tmp[threadIdx.x] - sum;
-  for (uint32_t k = 0; k < per; k++) {
-    if (b0 + k < nb) {
-      uint32_t v = a[b0 + k];
-      a[b0 + k] = run;
-      run += v;
-    }
-  }
-  __syncthreads();
-}
-
-// LDS layout: hist[nb] | lstart[nb] | gbase[nb] | tmp[256] | skey[RS_ST] | sval[RS_ST]
-template <class Load, class Bin, bool WRITE_KEY>
+// LDS layout: hist[nb] | lstart[nb] | gbase[nb] | tmp[4] | skey[RS_ST] | sval[RS_ST]
+// Four barriers per sub-tile; hist is zeroed by the caller's first barrier.
+template <int RS_ST, class Load, class Bin, bool WRITE_KEY>
 __device__ __forceinline__ void rs_scatter_tiles(uint32_t count, uint32_t nb, uint32_t* lds, Load load, Bin bin,
                                                  uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
   uint32_t* hist = lds;
@@ -233,22 +266,23 @@ __device__ __forceinline__ void rs_scatter_tiles(uint32_t count, uint32_t nb, ui
   uint32_t* tmp = lds + 3 * nb;
   uint32_t* skey = tmp + RS_THREADS;
   uint32_t* sval = skey + RS_ST;
+  constexpr int RS_PER = RS_ST / RS_THREADS;
+  for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) hist[x] = 0;
+  __syncthreads();
   for (uint32_t s0 = 0; s0 < count; s0 += RS_ST) {
-    for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) hist[x] = 0;
-    __syncthreads();
     uint32_t key[RS_PER], val[RS_PER], rk[RS_PER];
     bool ok[RS_PER];
 #pragma unroll
     for (int k = 0; k < RS_PER; k++) {
       uint32_t e = s0 + k * RS_THREADS + threadIdx.x;
       ok[k] = e < count && load(e, key[k], val[k]);
-      if (ok[k]) rk[k] = atomicAdd(&hist[bin(key[k])], 1u);
     }
+#pragma unroll
+    for (int k = 0; k < RS_PER; k++)
+      if (ok[k]) rk[k] = atomicAdd(&hist[bin(key[k])], 1u);
     __syncthreads();
-    for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) lstart[x] = hist[x];
+    const uint32_t total = rs_block_scan(hist, lstart, nb, tmp);
     __syncthreads();
-    rs_block_scan(lstart, nb, tmp);
-    uint32_t total = lstart[nb - 1] + hist[nb - 1];
 #pragma unroll
     for (int k = 0; k < RS_PER; k++) {
       if (ok[k]) {
@@ -265,13 +299,18 @@ __device__ __forceinline__ void rs_scatter_tiles(uint32_t count, uint32_t nb, ui
       oval[g] = sval[q];
     }
     __syncthreads();
-    for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) gbase[x] += hist[x];
+    for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) {
+      gbase[x] += hist[x];
+      hist[x] = 0;
+    }
     __syncthreads();
   }
 }
 
-__host__ __device__ constexpr size_t rs_scatter_lds(uint32_t nb) { return (3 * (size_t)nb + RS_THREADS + 2 * RS_ST) * 4; }
+// entries per LDS sub-tile: 4096 or 8192 (longer runs per bin, fewer resident workgroups)
+__host__ __device__ constexpr size_t rs_scatter_lds(uint32_t nb, uint32_t st) { return (3 * (size_t)nb + RS_THREADS + 2 * st) * 4; }
 
+template <int RS_ST>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_scatter(const int32_t* __restrict__ digits, uint64_t M,
                                                               uint32_t ne, uint32_t B, uint32_t NH, uint32_t lob,
                                                               uint32_t C1, uint32_t nc1, const uint32_t* __restrict__ offs1,
@@ -282,7 +321,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_scatter(const int32_t* __r
   const uint32_t count = (uint32_t)std::min<uint64_t>(C1, M - base);
   auto load = [&](uint32_t e, uint32_t& key, uint32_t& val) { return rs_key(digits, base + e, ne, B, key, val); };
   auto bin = [lob](uint32_t key) { return key >> lob; };
-  rs_scatter_tiles<decltype(load), decltype(bin), true>(count, NH, lds, load, bin, okey, oval);
+  rs_scatter_tiles<RS_ST, decltype(load), decltype(bin), true>(count, NH, lds, load, bin, okey, oval);
 }
 
 // one workgroup: bin starts and tile starts (tiles of <= C2 entries per bin)
@@ -351,12 +390,24 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p2_count(const uint32_t* __re
   const uint32_t lo = binstart[h] + q * C2, hi = min(lo + C2, binstart[h + 1]);
   for (uint32_t x = threadIdx.x; x < NLO; x += RS_THREADS) hist[x] = 0;
   __syncthreads();
-  for (uint32_t p = lo + threadIdx.x; p < hi; p += RS_THREADS) atomicAdd(&hist[okey[p] & mask], 1u);
+  constexpr int U = 8;  // loads in flight per thread
+  for (uint32_t p0 = lo; p0 < hi; p0 += U * RS_THREADS) {
+    uint32_t kk[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t p = p0 + u * RS_THREADS + threadIdx.x;
+      kk[u] = p < hi ? okey[p] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (kk[u] != 0xFFFFFFFFu) atomicAdd(&hist[kk[u] & mask], 1u);
+  }
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < NLO; x += RS_THREADS)
     cnt2[((size_t)tstart[h] << lob) + (size_t)x * nt + q] = hist[x];
 }
 
+template <int RS_ST>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p2_scatter(const uint32_t* __restrict__ okey,
                                                               const uint32_t* __restrict__ oval,
                                                               const uint32_t* __restrict__ binstart,
@@ -378,7 +429,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p2_scatter(const uint32_t* __
     return true;
   };
   auto bin = [mask](uint32_t key) { return key & mask; };
-  rs_scatter_tiles<decltype(load), decltype(bin), false>(hi - lo, NLO, lds, load, bin, nullptr, sval);
+  rs_scatter_tiles<RS_ST, decltype(load), decltype(bin), false>(hi - lo, NLO, lds, load, bin, nullptr, sval);
 }
 
 // bucket starts: start of key k = scanned count at (hi, lo, tile 0)
@@ -1715,14 +1766,17 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   // lo digit = the rest (8..13 bits) inside each hi bin (P2, XCD-local)
   uint32_t kb = 0;
   while ((1u << kb) < P.K) kb++;
-  const uint32_t lob = kb > 16 ? kb - 8 : 8;
+  static const int env_lob = [] { const char* e = getenv("ZKMI_RS_LOB"); return e ? atoi(e) : 0; }();
+  static const int env_c2 = [] { const char* e = getenv("ZKMI_RS_C2"); return e ? atoi(e) : 0; }();
+  const uint32_t lob = env_lob ? (uint32_t)env_lob : (kb > 16 ? kb - 8 : 8);
   const uint32_t NH = (P.K + (1u << lob) - 1) >> lob;
   const size_t Mmax = P.Mmax;
   // radix-sort geometry (see k_rs_*): ~2K P1 chunks, ~8K P2 tiles at most
   const uint32_t C1 = 16384u * (uint32_t)std::max<size_t>(1, (Mmax + 16384ull * 2048 - 1) / (16384ull * 2048));
   const uint32_t nc1 = (uint32_t)((Mmax + C1 - 1) / C1);
   const uint32_t C2b = std::max(8192u, 4u << lob);  // >= 4 entries per lo bin per tile
-  const uint32_t C2 = C2b * (uint32_t)std::max<size_t>(1, (Mmax + (size_t)C2b * 8192 - 1) / ((size_t)C2b * 8192));
+  const uint32_t C2 = env_c2 ? (uint32_t)env_c2
+                            : C2b * (uint32_t)std::max<size_t>(1, (Mmax + (size_t)C2b * 8192 - 1) / ((size_t)C2b * 8192));
   const uint32_t T2max = (uint32_t)((Mmax + C2 - 1) / C2) + NH;
   const size_t len1 = (size_t)NH * nc1, len2 = (size_t)T2max << lob;
   int32_t* digits;
@@ -1753,15 +1807,28 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   const uint32_t ne = (uint32_t)P.ne;
   k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1, cnt1);
   scan(cnt1, len1, &tot[0]);
-  k_rs_p1_scatter<<<nc1, RS_THREADS, rs_scatter_lds(NH), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1, cnt1, okey,
-                                                                oval);
+  static const int env_st1 = [] { const char* e = getenv("ZKMI_RS_ST1"); return e ? atoi(e) : 4096; }();
+  static const int env_st2 = [] { const char* e = getenv("ZKMI_RS_ST2"); return e ? atoi(e) : 0; }();
+  // P2 sub-tiles of 8192 entries (runs twice as long per lo bin) pay off for
+  // large sorts (2^26 table MSM: P2 scatter -1 ms) and lose on small ones
+  const int st2 = env_st2 ? env_st2 : (Mmax >= (size_t(1) << 26) ? 8192 : 4096);
+  if (env_st1 == 8192 && rs_scatter_lds(NH, 8192) <= 160 * 1024)
+    k_rs_p1_scatter<8192><<<nc1, RS_THREADS, rs_scatter_lds(NH, 8192), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1,
+                                                                               cnt1, okey, oval);
+  else
+    k_rs_p1_scatter<4096><<<nc1, RS_THREADS, rs_scatter_lds(NH, 4096), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1,
+                                                                               cnt1, okey, oval);
   k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, nc1, NH, &tot[0], C2, binstart, tstart);
   ZK_HIP(hipMemsetAsync(cnt2, 0, len2 * 4, st));
   const uint32_t g2 = ((T2max + 7) / 8) * 8;  // XCD-mapped grid (rs_xcd_tile)
   k_rs_p2_count<<<g2, RS_THREADS, (1u << lob) * 4, st>>>(okey, binstart, tstart, NH, lob, C2, T2max, cnt2);
   scan(cnt2, len2, &tot[1]);
   k_rs_bstart<<<(P.K + 256) / 256, 256, 0, st>>>(cnt2, binstart, tstart, NH, lob, P.K, bstart);
-  k_rs_p2_scatter<<<g2, RS_THREADS, rs_scatter_lds(1u << lob), st>>>(okey, oval, binstart, tstart, NH, lob, C2, T2max,
+  if (st2 == 8192 && rs_scatter_lds(1u << lob, 8192) <= 160 * 1024)
+    k_rs_p2_scatter<8192><<<g2, RS_THREADS, rs_scatter_lds(1u << lob, 8192), st>>>(okey, oval, binstart, tstart, NH, lob, C2, T2max,
+                                                                     cnt2, sval);
+  else
+    k_rs_p2_scatter<4096><<<g2, RS_THREADS, rs_scatter_lds(1u << lob, 4096), st>>>(okey, oval, binstart, tstart, NH, lob, C2, T2max,
                                                                      cnt2, sval);
   ZK_HIP(hipGetLastError());
   *out_sval = sval;
