@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--no-big", action="store_true", help="skip the config-5 global 2^26 MSM (sharded over all ranks)")
     ap.add_argument("--big-log-n", type=int, default=26, help="global MSM size 2^k of the config-5 measurement")
     ap.add_argument("--big-steps", type=int, default=5)
+    ap.add_argument("--lanes", type=int, default=3,
+                    help="MSM lanes (streams with private scratch) = MSMs kept in flight in the timed loops")
     return ap.parse_args()
 
 
@@ -101,16 +103,11 @@ def main():
             return combine_partials(part, _coll_dev)
         return part
 
+    ctx.set_lanes(args.lanes)
+
     def run(k):
-        """k MSM steps, pipelined: submit step i+1 before finishing step i."""
-        if k <= 0:
-            return None
-        pending = ctx.msm_submit(bases, scalars, n)
-        for _ in range(k - 1):
-            nxt = ctx.msm_submit(bases, scalars, n)
-            finish(pending)
-            pending = nxt
-        return finish(pending)
+        """k MSM steps, pipelined: args.lanes MSMs in flight, one per lane."""
+        return pipelined(lambda: ctx.msm_submit(bases, scalars, n), finish, k, args.lanes)
 
     def timed(k, warm):
         run(warm)
@@ -160,7 +157,7 @@ def main():
     ovl_tot, ovl_cnt = ctx.profile_get(kernel)
     # Roofline pass: the dominant kernel timed in isolation (one lane, each MSM
     # finished before the next), HIP events on the lane stream it runs on.  In
-    # the timed region two lanes overlap, which stretches every kernel's span.
+    # the timed region several lanes overlap, which stretches every kernel's span.
     rf_launches = 5
     ctx.set_lanes(1)
     ctx.profile(True)
@@ -169,7 +166,7 @@ def main():
         ctx.msm(bases, scalars)
     ktot, kcnt = ctx.profile_get(kernel)
     ctx.profile(False)
-    ctx.set_lanes(2)
+    ctx.set_lanes(args.lanes)
     kavg_s = ktot / max(kcnt, 1) / 1e3
     achieved = MSM_BYTES_PER_PAIR * n / kavg_s / 1e9 if kcnt else None
     # acc0_g1 launches before the roofline pass (for tools/rocpd_summary.py)
@@ -177,10 +174,14 @@ def main():
     pairs_total = n * world * args.steps
     value = pairs_total / elapsed / 1e6
 
-    extra = {"msm_stage_ms_per_step": breakdown, "fixed_base_table": table, "msm_plain_no_table": plain}
+    extra = {"msm_stage_ms_per_step": breakdown, "fixed_base_table": table, "msm_plain_no_table": plain,
+             "lanes": args.lanes}
+    # side measurements below: 2 lanes (the 2^26 MSM and the provers measured
+    # best there: their MSMs are long enough that two overlap fully)
+    ctx.set_lanes(2)
     if not args.no_big:
         extra["msm_global_2_%d" % args.big_log_n] = bench_msm_sharded(
-            ctx, args.big_log_n, args.big_steps, world, rank, dist, finish, sync_all, _coll_dev)
+            ctx, args.big_log_n, args.big_steps, world, rank, dist, finish, sync_all, _coll_dev, 2)
     if rank == 0 and world == 1 and not args.no_ntt:
         extra["ntt"] = bench_ntt(ctx, args.ntt_log_n)
     if rank == 0 and world == 1 and not args.no_l2:
@@ -238,7 +239,7 @@ def main():
             "kernel_avg_ms_in_timed_region": round(ovl_tot / max(ovl_cnt, 1), 4),
             "algorithmic_bytes_per_launch": MSM_BYTES_PER_PAIR * n,
             "note": "MSM is VALU-bound (256-bit modular multiplies), not HBM-bound; frac is vs HBM peak as BASELINE.md "
-                    "defines. kernel_avg_ms = isolated launches (one lane); the timed region runs two lanes whose "
+                    "defines. kernel_avg_ms = isolated launches (one lane); the timed region runs " + str(args.lanes) + " lanes whose "
                     "kernels overlap",
         },
         "valu_roofline": valu,
@@ -252,7 +253,22 @@ def main():
         dist.destroy_process_group()
 
 
-def bench_msm_sharded(ctx, log_total, steps, world, rank, dist, finish, sync_all, coll_dev):
+def pipelined(submit, finish, k, depth):
+    """k MSMs with `depth` of them in flight (submit i + depth - 1 before
+    finishing i); returns the last result."""
+    from collections import deque
+
+    q, res = deque(), None
+    for _ in range(k):
+        q.append(submit())
+        if len(q) >= depth:
+            res = finish(q.popleft())
+    while q:
+        res = finish(q.popleft())
+    return res
+
+
+def bench_msm_sharded(ctx, log_total, steps, world, rank, dist, finish, sync_all, coll_dev, lanes=2):
     """BASELINE.json configs[4]: ONE global BN254 G1 MSM of 2^log_total
     point-scalar pairs, point-sharded over the world's ranks (strong scaling:
     rank r owns elements [r*N/W, (r+1)*N/W) of the same global set, resident
@@ -272,12 +288,7 @@ def bench_msm_sharded(ctx, log_total, steps, world, rank, dist, finish, sync_all
     table_s = time.perf_counter() - t0
 
     def run(k):
-        pending = ctx.msm_submit(bases, scalars, per)
-        for _ in range(k - 1):
-            nxt = ctx.msm_submit(bases, scalars, per)
-            finish(pending)
-            pending = nxt
-        return finish(pending)
+        return pipelined(lambda: ctx.msm_submit(bases, scalars, per), finish, k, lanes)
 
     run(1)
     sync_all()
