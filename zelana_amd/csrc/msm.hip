@@ -1648,7 +1648,11 @@ int table_window(size_t N, int g2) {
   (void)g2;
   int best = 8;
   double cost = 1e300;
-  for (int c = 6; c <= 20; c++) {
+  // c = 22 (12 copies instead of 13, 2^21 buckets) from 2^25 bases on: 2^26
+  // one lane 73.8 -> 72.8 ms, two lanes 914 -> 942 Mpoint/s; below that its
+  // latency-bound bucket reduction (~1 ms) costs more than it saves
+  const int cmax = N >= (size_t(1) << 25) ? 22 : 20;
+  for (int c = 6; c <= cmax; c++) {
     double k = (double)msm_windows(c) * (double)N + 2.5 * (double)(1u << (c - 1));
     if (k < cost) {
       cost = k;
@@ -1768,7 +1772,8 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   while ((1u << kb) < P.K) kb++;
   static const int env_lob = [] { const char* e = getenv("ZKMI_RS_LOB"); return e ? atoi(e) : 0; }();
   static const int env_c2 = [] { const char* e = getenv("ZKMI_RS_C2"); return e ? atoi(e) : 0; }();
-  const uint32_t lob = env_lob ? (uint32_t)env_lob : (kb > 16 ? kb - 8 : 8);
+  // 21-bit keys (c = 22 tables): 9 hi bits, 12 lo (2^26: 0.8 ms faster than 8 + 13)
+  const uint32_t lob = env_lob ? (uint32_t)env_lob : (kb > 20 ? kb - 9 : kb > 16 ? kb - 8 : 8);
   const uint32_t NH = (P.K + (1u << lob) - 1) >> lob;
   const size_t Mmax = P.Mmax;
   // radix-sort geometry (see k_rs_*): ~2K P1 chunks, ~8K P2 tiles at most
