@@ -257,34 +257,29 @@ __device__ __forceinline__ uint32_t rs_block_scan(const uint32_t* hist, uint32_t
 // written lines get evicted (measured: ~10x slower than the reads).
 // LDS layout: hist[nb] | lstart[nb] | gbase[nb] | tmp[4] | skey[RS_ST] | sval[RS_ST]
 // Four barriers per sub-tile; hist is zeroed by the caller's first barrier.
-template <int RS_ST, class Load, class Bin, bool WRITE_KEY>
-__device__ __forceinline__ void rs_scatter_tiles(uint32_t count, uint32_t nb, uint32_t* lds, Load load, Bin bin,
+template <int PER, class Fill, class Bin, bool WRITE_KEY>
+__device__ __forceinline__ void rs_scatter_core(uint32_t nsub, uint32_t nb, uint32_t* lds, Fill fill, Bin bin,
                                                  uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
   uint32_t* hist = lds;
   uint32_t* lstart = lds + nb;
   uint32_t* gbase = lds + 2 * nb;
   uint32_t* tmp = lds + 3 * nb;
   uint32_t* skey = tmp + RS_THREADS;
-  uint32_t* sval = skey + RS_ST;
-  constexpr int RS_PER = RS_ST / RS_THREADS;
+  uint32_t* sval = skey + PER * RS_THREADS;
   for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) hist[x] = 0;
   __syncthreads();
-  for (uint32_t s0 = 0; s0 < count; s0 += RS_ST) {
-    uint32_t key[RS_PER], val[RS_PER], rk[RS_PER];
-    bool ok[RS_PER];
+  for (uint32_t sub = 0; sub < nsub; sub++) {
+    uint32_t key[PER], val[PER], rk[PER];
+    bool ok[PER];
+    fill(sub, key, val, ok);
 #pragma unroll
-    for (int k = 0; k < RS_PER; k++) {
-      uint32_t e = s0 + k * RS_THREADS + threadIdx.x;
-      ok[k] = e < count && load(e, key[k], val[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < RS_PER; k++)
+    for (int k = 0; k < PER; k++)
       if (ok[k]) rk[k] = atomicAdd(&hist[bin(key[k])], 1u);
     __syncthreads();
     const uint32_t total = rs_block_scan(hist, lstart, nb, tmp);
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < RS_PER; k++) {
+    for (int k = 0; k < PER; k++) {
       if (ok[k]) {
         uint32_t lp = lstart[bin(key[k])] + rk[k];
         skey[lp] = key[k];
@@ -307,6 +302,21 @@ __device__ __forceinline__ void rs_scatter_tiles(uint32_t count, uint32_t nb, ui
   }
 }
 
+// entries e in [0, count) from load(e, key, val), RS_ST per sub-tile
+template <int RS_ST, class Load, class Bin, bool WRITE_KEY>
+__device__ __forceinline__ void rs_scatter_tiles(uint32_t count, uint32_t nb, uint32_t* lds, Load load, Bin bin,
+                                                 uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+  constexpr int PER = RS_ST / RS_THREADS;
+  auto fill = [&](uint32_t sub, uint32_t* key, uint32_t* val, bool* ok) {
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t e = sub * RS_ST + k * RS_THREADS + threadIdx.x;
+      ok[k] = e < count && load(e, key[k], val[k]);
+    }
+  };
+  rs_scatter_core<PER, decltype(fill), Bin, WRITE_KEY>((count + RS_ST - 1) / RS_ST, nb, lds, fill, bin, okey, oval);
+}
+
 // entries per LDS sub-tile: 4096 or 8192 (longer runs per bin, fewer resident workgroups)
 __host__ __device__ constexpr size_t rs_scatter_lds(uint32_t nb, uint32_t st) { return (3 * (size_t)nb + RS_THREADS + 2 * st) * 4; }
 
@@ -322,6 +332,76 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_scatter(const int32_t* __r
   auto load = [&](uint32_t e, uint32_t& key, uint32_t& val) { return rs_key(digits, base + e, ne, B, key, val); };
   auto bin = [lob](uint32_t key) { return key >> lob; };
   rs_scatter_tiles<RS_ST, decltype(load), decltype(bin), true>(count, NH, lds, load, bin, okey, oval);
+}
+
+// P1 straight from the scalars (windows c >= 12, W <= 22): one thread takes
+// one scalar and its W signed digits, i.e. entries (w' * p + j) * n + i of the
+// digit layout of k_msm_digits (key w' * B + |d| - 1, value (j * n + i) | sign);
+// a P1 chunk is CS scalars.  No digits array: its write and two reads go
+// (2^26 table MSM: 3.2 GB written + 6.4 GB read).
+template <int C>
+__device__ __forceinline__ void rs_scalar_keys(const uint32_t* __restrict__ scalars, size_t i, size_t n, int Wp,
+                                               uint32_t B, uint32_t* key, uint32_t* val, bool* ok) {
+  constexpr int W = msm_windows(C);
+  int32_t d[W];
+  scalar_digits<C>(scalars, i, d);
+  uint32_t j = 0, wq = 0;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    const int32_t v = d[w];
+    ok[w] = v != 0;
+    key[w] = wq * B + (uint32_t)(v < 0 ? -v : v) - 1;
+    val[w] = (uint32_t)(j * n + i) | (v < 0 ? 0x80000000u : 0u);
+    if (++wq == (uint32_t)Wp) {
+      wq = 0;
+      j++;
+    }
+  }
+}
+
+template <int C>
+__global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_count(const uint32_t* __restrict__ scalars, size_t n, int Wp,
+                                                             uint32_t B, uint32_t NH, uint32_t lob, uint32_t CS,
+                                                             uint32_t nc1, uint32_t* __restrict__ cnt1) {
+  extern __shared__ uint32_t hist[];
+  constexpr int W = msm_windows(C);
+  for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) hist[x] = 0;
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * CS;
+  for (uint32_t k = threadIdx.x; k < CS && base + k < n; k += RS_THREADS) {
+    uint32_t key[W], val[W];
+    bool ok[W];
+    rs_scalar_keys<C>(scalars, base + k, n, Wp, B, key, val, ok);
+#pragma unroll
+    for (int w = 0; w < W; w++)
+      if (ok[w]) atomicAdd(&hist[key[w] >> lob], 1u);
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) cnt1[(size_t)x * nc1 + blockIdx.x] = hist[x];
+}
+
+template <int C>
+__global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_scatter(const uint32_t* __restrict__ scalars, size_t n, int Wp,
+                                                               uint32_t B, uint32_t NH, uint32_t lob, uint32_t CS,
+                                                               uint32_t nc1, const uint32_t* __restrict__ offs1,
+                                                               uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+  extern __shared__ uint32_t lds[];
+  constexpr int W = msm_windows(C);
+  for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) lds[2 * NH + x] = offs1[(size_t)x * nc1 + blockIdx.x];
+  const size_t base = (size_t)blockIdx.x * CS;
+  const uint32_t cnt = (uint32_t)std::min<size_t>(CS, n - base);
+  auto fill = [&](uint32_t sub, uint32_t* key, uint32_t* val, bool* ok) {
+    const uint32_t k = sub * RS_THREADS + threadIdx.x;
+    if (k < cnt) {
+      rs_scalar_keys<C>(scalars, base + k, n, Wp, B, key, val, ok);
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; w++) ok[w] = false;
+    }
+  };
+  auto bin = [lob](uint32_t key) { return key >> lob; };
+  rs_scatter_core<W, decltype(fill), decltype(bin), true>((cnt + RS_THREADS - 1) / RS_THREADS, NH, lds, fill, bin,
+                                                          okey, oval);
 }
 
 // one workgroup: bin starts and tile starts (tiles of <= C2 entries per bin)
@@ -1690,6 +1770,30 @@ static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, size_t n, 
   return 0;
 }
 
+template <int C>
+static void launch_p1_fused(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t NH,
+                            uint32_t lob, uint32_t CS, uint32_t nf, uint32_t* cnt1, uint32_t* okey, uint32_t* oval,
+                            bool scatter) {
+  if (scatter)
+    k_rs_p1f_scatter<C><<<nf, RS_THREADS, rs_scatter_lds(NH, RS_THREADS * msm_windows(C)), st>>>(
+        sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval);
+  else
+    k_rs_p1f_count<C><<<nf, RS_THREADS, NH * 4, st>>>(sc, n, Wp, B, NH, lob, CS, nf, cnt1);
+}
+static int p1_fused(int c, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t NH, uint32_t lob,
+                    uint32_t CS, uint32_t nf, uint32_t* cnt1, uint32_t* okey, uint32_t* oval, bool scatter) {
+  switch (c) {
+#define ZK_C(CC) \
+  case CC: launch_p1_fused<CC>(st, sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval, scatter); break;
+    ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15) ZK_C(16) ZK_C(17) ZK_C(18) ZK_C(19) ZK_C(20) ZK_C(21) ZK_C(22)
+#undef ZK_C
+    default:
+      set_error("p1_fused: unsupported MSM window %d", c);
+      return ZKMI_EINVAL;
+  }
+  return 0;
+}
+
 }  // namespace zk
 
 // An MSM in flight: GPU work and the D2H of the bit sums are queued on the
@@ -1783,10 +1887,15 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   const uint32_t C2 = env_c2 ? (uint32_t)env_c2
                             : C2b * (uint32_t)std::max<size_t>(1, (Mmax + (size_t)C2b * 8192 - 1) / ((size_t)C2b * 8192));
   const uint32_t T2max = (uint32_t)((Mmax + C2 - 1) / C2) + NH;
-  const size_t len1 = (size_t)NH * nc1, len2 = (size_t)T2max << lob;
+  // fused P1: chunks of CS scalars (~2K chunks at most)
+  const uint32_t CS = 1024u * (uint32_t)std::max<size_t>(1, (n + 1024ull * 2048 - 1) / (1024ull * 2048));
+  const uint32_t nf = (uint32_t)std::max<size_t>(1, (n + CS - 1) / CS);
+  const size_t len1 = (size_t)NH * std::max(nc1, nf), len2 = (size_t)T2max << lob;
   int32_t* digits;
   uint32_t *bstart, *sval, *cnt1, *okey, *oval, *binstart, *tstart, *cnt2, *bsums, *tot;
-  ZK_TRY(ws.get("msm_digits", Mmax * 4, (void**)&digits));
+  const bool fused = P.c >= 12 && P.c <= 22;  // P1 reads the scalars (k_rs_p1f_*)
+  digits = nullptr;
+  if (!fused) ZK_TRY(ws.get("msm_digits", Mmax * 4, (void**)&digits));
   ZK_TRY(ws.get("msm_bstart", (size_t)(P.K + 1) * 4, (void**)&bstart));
   ZK_TRY(ws.get("msm_sval", Mmax * 4, (void**)&sval));
   ZK_TRY(ws.get("msm_okey", Mmax * 4, (void**)&okey));
@@ -1800,31 +1909,42 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   ZK_HIP(hipEventRecord(lane->fork, ctx->stream));
   ZK_HIP(hipStreamWaitEvent(st, lane->fork, 0));
   ScopedKernelTimer tm(ctx, "msm_sort", st);
-  ZK_TRY(dispatch_digits(P.c, st, d_scalars, n, P.p, P.W, digits));
-  ZK_HIP(hipEventRecord(lane->consumed, st));
-  ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
+  if (!fused) {
+    ZK_TRY(dispatch_digits(P.c, st, d_scalars, n, P.p, P.W, digits));
+    ZK_HIP(hipEventRecord(lane->consumed, st));
+    ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
+  }
   auto scan = [&](uint32_t* a, size_t len, uint32_t* total) {
     uint32_t nb = (uint32_t)((len + 1023) / 1024);
     k_scan_blocks<<<nb, 256, 0, st>>>(a, (uint32_t)len, a, bsums);
     k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, total);
     k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
   };
-  const uint32_t ne = (uint32_t)P.ne;
-  k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1, cnt1);
-  scan(cnt1, len1, &tot[0]);
   static const int env_st1 = [] { const char* e = getenv("ZKMI_RS_ST1"); return e ? atoi(e) : 4096; }();
   static const int env_st2 = [] { const char* e = getenv("ZKMI_RS_ST2"); return e ? atoi(e) : 0; }();
   // P2 sub-tiles of 8192 entries (runs twice as long per lo bin) pay off for
   // large sorts (2^26 table MSM: P2 scatter -1 ms) and lose on small ones
   const int st2 = env_st2 ? env_st2 : (Mmax >= (size_t(1) << 26) ? 8192 : 4096);
-  if (env_st1 == 8192 && rs_scatter_lds(NH, 8192) <= 160 * 1024)
+  const uint32_t ne = (uint32_t)P.ne;
+  if (fused) {
+    ZK_TRY(p1_fused(P.c, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, nullptr, nullptr, false));
+    scan(cnt1, (size_t)NH * nf, &tot[0]);
+    ZK_TRY(p1_fused(P.c, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, okey, oval, true));
+    ZK_HIP(hipEventRecord(lane->consumed, st));
+    ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
+  } else {
+    k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1, cnt1);
+    scan(cnt1, len1, &tot[0]);
+    if (env_st1 == 8192 && rs_scatter_lds(NH, 8192) <= 160 * 1024)
     k_rs_p1_scatter<8192><<<nc1, RS_THREADS, rs_scatter_lds(NH, 8192), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1,
                                                                                cnt1, okey, oval);
   else
     k_rs_p1_scatter<4096><<<nc1, RS_THREADS, rs_scatter_lds(NH, 4096), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1,
                                                                                cnt1, okey, oval);
-  k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, nc1, NH, &tot[0], C2, binstart, tstart);
-  ZK_HIP(hipMemsetAsync(cnt2, 0, len2 * 4, st));
+  }
+  k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, fused ? nf : nc1, NH, &tot[0], C2, binstart, tstart);
+  // cnt2 needs no clearing: tiles t < tstart[NH] write all their counts, and
+  // the stale tail after them only reaches the (unused) scan total
   const uint32_t g2 = ((T2max + 7) / 8) * 8;  // XCD-mapped grid (rs_xcd_tile)
   k_rs_p2_count<<<g2, RS_THREADS, (1u << lob) * 4, st>>>(okey, binstart, tstart, NH, lob, C2, T2max, cnt2);
   scan(cnt2, len2, &tot[1]);
