@@ -433,6 +433,10 @@ def bench_zbatch(ctx, steps):
     d = zbatch.load_prover_toml(os.path.join(ROOT, "tests", "golden", "zelana_batch_70_Prover.toml"))
     cs, z, _ = zbatch.build(d)
     synth_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    _, zw, _ = zbatch.build(d, witness_only=True)  # per batch: the R1CS and key are fixed
+    witness_s = time.perf_counter() - t0
+    assert np.array_equal(zw, z)
     log_n = 0
     while (1 << log_n) < cs.num_constraints + cs.num_instance:
         log_n += 1
@@ -462,7 +466,9 @@ def bench_zbatch(ctx, steps):
                     f"constraints, {cs.num_variables} variables, domain 2^{log_n}; r, s from StdRng(batch_id)",
         "proofs_per_s": round(1.0 / dt, 3),
         "ms_per_proof": round(dt * 1e3, 2),
-        "witness_synthesis_s_host_python": round(synth_s, 2),
+        "r1cs_and_witness_synthesis_s_host": round(synth_s, 2),
+        "witness_s_per_batch_host": round(witness_s, 3),
+        "witness_native_mimc": zbatch._native_mimc() is not None,
         "keygen_s_gpu": round(keygen_s, 3),
         "table_and_upload_s": round(setup_s, 2),
         "note": "real proving key (GPU circuit_specific_setup, StdRng(0) as keygen.rs); witness resident in HBM",

@@ -82,3 +82,40 @@ def test_synthetic_batches(depth, ntx):
         assert computed[k] == d[k] % Z.R, k
     st, keep = O.make_r1cs(cs)
     assert O.lib().oracle_r1cs_check(ctypes.byref(st), O.P(z)) == -1
+
+
+def _python_only(monkeypatch):
+    monkeypatch.setenv("ZKMI_ZBATCH_PY", "1")
+    monkeypatch.setattr(Z, "_NATIVE", False)
+
+
+def test_native_mimc_matches_python(monkeypatch):
+    """libzelana_prover.so's MiMC (host/mimc.cpp) == the Python restatement:
+    permute(x, k) on edge values and the per-round trace Builder.permute records."""
+    assert Z._native_mimc() is not None, "libzelana_prover.so not built"
+    xs = [0, 1, 2, Z.R - 1, Z.R - 2, 1 << 253, 12345678901234567890]
+    nat = [Z.mimc_permute(x, k) for x in xs for k in (0, 1, Z.R - 1)]
+    bn = Z.Builder()
+    vn = bn.permute(bn.witness(987654321))
+    _python_only(monkeypatch)
+    assert Z._native_mimc() is None
+    assert nat == [Z.mimc_permute(x, k) for x in xs for k in (0, 1, Z.R - 1)]
+    bp = Z.Builder()
+    vp = bp.permute(bp.witness(987654321))
+    assert vn.v == vp.v and vn.t == vp.t
+    assert np.array_equal(bn.assignment(), bp.assignment())
+
+
+@pytest.mark.parametrize("depth,ntx", [(4, 3)])
+def test_witness_only_and_native_equal_python(monkeypatch, depth, ntx):
+    d = Z.synthetic_batch(depth, ntx, seed=7)
+    kw = dict(max_transfers=ntx, max_withdrawals=1, max_shielded=1, depth=depth)
+    cs, z, computed = Z.build(d, **kw)
+    _, zw, cw = Z.build(d, witness_only=True, **kw)
+    assert np.array_equal(z, zw) and cw == computed
+    _python_only(monkeypatch)
+    cs2, z2, computed2 = Z.build(d, **kw)
+    assert np.array_equal(z, z2) and computed == computed2
+    for name in ("a", "b", "c"):
+        for x, y in zip(cs.csr(name), cs2.csr(name)):
+            assert np.array_equal(x, y), name

@@ -36,6 +36,9 @@ batch_hash equal its public inputs (tests/test_zbatch.py).
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import numpy as np
 
 from .r1cs import R1CS, R
@@ -49,7 +52,40 @@ PUBLIC = ("pre_state_root", "post_state_root", "pre_shielded_root", "post_shield
 
 
 # ----------------------------------------------------------------- host MiMC
+def _native_mimc():
+    """libzelana_prover.so's MiMC (zelana_amd/host/mimc.cpp), or None when the
+    host library is not built (or ZKMI_ZBATCH_PY=1): the Python below is then
+    the witness path, with identical values (tests/test_zbatch.py)."""
+    global _NATIVE
+    if _NATIVE is False:
+        _NATIVE = None
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libzelana_prover.so")
+        if os.path.exists(path) and os.environ.get("ZKMI_ZBATCH_PY") != "1":
+            L = ctypes.CDLL(path)
+            L.zp_mimc_permute.argtypes = [ctypes.c_void_p] * 3
+            L.zp_mimc_trace.argtypes = [ctypes.c_void_p] * 2
+            assert L.zp_mimc_rounds() == MIMC_ROUNDS
+            _NATIVE = L
+    return _NATIVE
+
+
+_NATIVE = False
+
+
+def _limbs(x: int) -> np.ndarray:
+    return np.frombuffer(x.to_bytes(32, "little"), np.uint64)
+
+
+def _int(a: np.ndarray) -> int:
+    return int.from_bytes(a.tobytes(), "little")
+
+
 def mimc_permute(x: int, k: int = 0) -> int:
+    L = _native_mimc()
+    if L is not None:
+        xa, ka, y = _limbs(x % R), _limbs(k % R), np.empty(4, np.uint64)
+        L.zp_mimc_permute(xa.ctypes.data, ka.ctypes.data, y.ctypes.data)
+        return _int(y)
     for c in RC:
         t = (x + k + c) % R
         t2 = t * t % R
@@ -129,21 +165,36 @@ class Builder:
     as explicit rows."""
 
     def __init__(self):
+        # values in variable order: lists of ints, and (4*91, 4) u64 arrays
+        # for native MiMC traces; `vals` is the open int list
         self.vals = [1]
+        self.parts = [self.vals]
+        self.nv = 1
         self.num_instance = 1
         self.rows = {"a": [], "b": [], "c": []}
         self.perms = []  # (first variable, input terms)
 
     # variables
     def instance(self, value: int) -> LC:
-        assert len(self.vals) == self.num_instance, "instance variables come first"
-        self.vals.append(value % R)
+        assert self.nv == self.num_instance, "instance variables come first"
         self.num_instance += 1
-        return LC([(len(self.vals) - 1, 1)], value)
+        return self.witness(value)
 
     def witness(self, value: int) -> LC:
         self.vals.append(value % R)
-        return LC([(len(self.vals) - 1, 1)], value)
+        self.nv += 1
+        return LC([(self.nv - 1, 1)], value)
+
+    def set_value(self, var: int, value: int):
+        """Overwrite an int-held value (instance variables: public_from_witness)."""
+        base = 0
+        for part in self.parts:
+            if var < base + len(part):
+                assert isinstance(part, list), "variable belongs to a MiMC trace"
+                part[var - base] = value % R
+                return
+            base += len(part)
+        raise IndexError(var)
 
     def enforce(self, a: LC, b: LC, c: LC):
         self.rows["a"].append(a.t)
@@ -186,9 +237,20 @@ class Builder:
     def permute(self, x: LC) -> LC:
         if x.is_const():
             return const(mimc_permute(x.v))
-        v0 = len(self.vals)
+        v0 = self.nv
+        L = _native_mimc()
+        if L is not None:
+            tr = np.empty((4 * MIMC_ROUNDS, 4), np.uint64)
+            xa = _limbs(x.v)  # held: ctypes.data does not keep the array alive
+            L.zp_mimc_trace(xa.ctypes.data, tr.ctypes.data)
+            self.vals = []
+            self.parts += [tr, self.vals]
+            self.nv += 4 * MIMC_ROUNDS
+            self.perms.append((v0, x.t))
+            return LC([(v0 + 4 * MIMC_ROUNDS - 1, 1)], _int(tr[-1]))
         t = x.v
         vals = self.vals
+        self.nv += 4 * MIMC_ROUNDS
         for c in RC:
             t = (t + c) % R
             t2 = t * t % R
@@ -215,7 +277,7 @@ class Builder:
 
     # assembly
     def to_r1cs(self) -> tuple[R1CS, np.ndarray]:
-        nv = len(self.vals)
+        nv = self.nv
         cs = R1CS(self.num_instance, nv - self.num_instance)
         P = len(self.perms)
         ng = len(self.rows["a"])
@@ -263,8 +325,16 @@ class Builder:
                 col = np.zeros(1, np.uint64)
             cs.set_csr(name, rp, col, val)
         cs._m = m
-        z = np.frombuffer(b"".join(v.to_bytes(32, "little") for v in self.vals), np.uint64).reshape(-1, 4).copy()
-        return cs, z
+        return cs, self.assignment()
+
+    def assignment(self) -> np.ndarray:
+        """z as (num_variables, 4) canonical u64 limbs."""
+        nv = self.nv
+        z = np.concatenate([p if isinstance(p, np.ndarray) else
+                            np.frombuffer(b"".join(v.to_bytes(32, "little") for v in p), np.uint64).reshape(-1, 4)
+                            for p in self.parts if len(p)])
+        assert z.shape == (nv, 4)
+        return z
 
 
 def _perm_rows(name, v0, t0, rc_id, one_id, cid):
@@ -332,13 +402,15 @@ def _f(x) -> int:
 
 
 def build(prover: dict, max_transfers=MAX_TRANSFERS, max_withdrawals=MAX_WITHDRAWALS, max_shielded=MAX_SHIELDED,
-          public_from_witness: bool = False, depth: int = TREE_DEPTH):
+          public_from_witness: bool = False, depth: int = TREE_DEPTH, witness_only: bool = False):
     """R1CS + full assignment z for a Prover.toml-shaped dict (main.nr:112-357).
 
     public_from_witness: set the 7 public inputs to the values the witness
     computes (for reduced circuits); otherwise they are taken from `prover`
     and the final asserts only hold if the witness reproduces them.
-    Returns (cs, z, computed) with computed = the 7 recomputed public values."""
+    Returns (cs, z, computed) with computed = the 7 recomputed public values.
+    witness_only: skip the matrices (cs is None) — per-batch proving, where the
+    circuit's R1CS (and its key) are fixed."""
     b = Builder()
     pub = {k: b.instance(_f(prover.get(k, 0))) for k in PUBLIC}
     batch_id = pub["batch_id"]
@@ -453,12 +525,14 @@ def build(prover: dict, max_transfers=MAX_TRANSFERS, max_withdrawals=MAX_WITHDRA
                 "withdrawal_root": final_wd.v, "batch_hash": final_batch.v, "batch_id": batch_id.v}
     if public_from_witness:
         for k, lc in pub.items():
-            b.vals[lc.t[0][0]] = computed[k]
+            b.set_value(lc.t[0][0], computed[k])
             lc.v = computed[k]
     b.assert_eq(cur_root, pub["post_state_root"])  # main.nr:353-356
     b.assert_eq(cur_sh, pub["post_shielded_root"])
     b.assert_eq(final_wd, pub["withdrawal_root"])
     b.assert_eq(final_batch, pub["batch_hash"])
+    if witness_only:
+        return None, b.assignment(), computed
     cs, z = b.to_r1cs()
     return cs, z, computed
 
