@@ -86,7 +86,7 @@ def _build_host(verbose: bool):
         deps = cmd_srcs + hdrs + [LIB]
         if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
             continue
-        cmd = ["g++", "-O2", "-std=c++17", "-Wall"] + kind + inc + ["-o", out] + cmd_srcs + link
+        cmd = ["g++", "-O3", "-std=c++17", "-Wall"] + kind + inc + ["-o", out] + cmd_srcs + link
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("host build failed: " + " ".join(cmd) + "\n" + r.stdout + r.stderr)
