@@ -119,3 +119,13 @@ def test_witness_only_and_native_equal_python(monkeypatch, depth, ntx):
     for name in ("a", "b", "c"):
         for x, y in zip(cs.csr(name), cs2.csr(name)):
             assert np.array_equal(x, y), name
+
+
+def test_batch70_native_witness_equals_python(monkeypatch):
+    """Full batch 70 (1.42M variables): native MiMC traces + witness_only == the
+    Python restatement's assignment."""
+    d = _batch70()
+    _, zn, cn = Z.build(d, witness_only=True)
+    _python_only(monkeypatch)
+    _, zp, cp = Z.build(d, witness_only=True)
+    assert cn == cp and np.array_equal(zn, zp)
