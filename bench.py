@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--no-big", action="store_true", help="skip the config-5 global 2^26 MSM (sharded over all ranks)")
     ap.add_argument("--big-log-n", type=int, default=26, help="global MSM size 2^k of the config-5 measurement")
     ap.add_argument("--big-steps", type=int, default=5)
+    ap.add_argument("--depth", type=int, default=0,
+                    help="MSMs in flight in the headline (default: --lanes); above it, lanes queue a second MSM")
+    ap.add_argument("--timers-in-timed-region", action="store_true",
+                    help="keep the HIP-event stage timers on while timing the headline (default: separate pass)")
     ap.add_argument("--lanes", type=int, default=3,
                     help="MSM lanes (streams with private scratch) = MSMs kept in flight in the timed loops")
     return ap.parse_args()
@@ -107,12 +111,14 @@ def main():
 
     def run(k):
         """k MSM steps, pipelined: args.lanes MSMs in flight, one per lane."""
-        return pipelined(lambda: ctx.msm_submit(bases, scalars, n), finish, k, args.lanes)
+        return pipelined(lambda: ctx.msm_submit(bases, scalars, n), finish, k, args.depth or args.lanes)
 
-    def timed(k, warm):
+    def timed(k, warm, prof=False):
+        """prof: HIP-event stage timers on (the stage breakdown comes from a
+        separate profiled pass: the timers' events cost throughput)."""
         run(warm)
         sync_all()
-        ctx.profile(True)
+        ctx.profile(prof)
         ctx.profile_reset()
         sync_all()
         t0 = time.perf_counter()
@@ -139,6 +145,7 @@ def main():
     if not args.no_plain:
         psteps = max(1, args.steps // 2)
         pres, pdt = timed(psteps, 1)
+        timed(psteps, 0, prof=True)
         plain = {"value": round(n * world * psteps / pdt / 1e6, 2), "ms_per_step": round(pdt / psteps * 1e3, 4),
                  "stage_ms_per_step": stages(psteps)}
     table = None
@@ -148,7 +155,9 @@ def main():
         table = {"window": info[1], "copies": info[2], "windows": info[3],
                  "build_s": round(time.perf_counter() - t0, 3),
                  "hbm_bytes": info[2] * n * 64}
-    result, elapsed = timed(args.steps, args.warmup)
+    result, elapsed = timed(args.steps, args.warmup, prof=args.timers_in_timed_region)
+    if not args.timers_in_timed_region:
+        _, prof_elapsed = timed(args.steps, 0, prof=True)
     if plain is not None:
         plain["same_result"] = bool(np.array_equal(pres, result))
 
@@ -170,7 +179,8 @@ def main():
     kavg_s = ktot / max(kcnt, 1) / 1e3
     achieved = MSM_BYTES_PER_PAIR * n / kavg_s / 1e9 if kcnt else None
     # acc0_g1 launches before the roofline pass (for tools/rocpd_summary.py)
-    rf_first = (0 if args.no_plain else 1 + max(1, args.steps // 2)) + args.warmup + args.steps
+    rf_first = ((0 if args.no_plain else 1 + 2 * max(1, args.steps // 2)) + args.warmup
+                + args.steps * (1 if args.timers_in_timed_region else 2))
     pairs_total = n * world * args.steps
     value = pairs_total / elapsed / 1e6
 
