@@ -7,6 +7,9 @@
 // in the order zbatch.Builder.permute allocates them, so the Python front-end
 // spends no big-integer arithmetic on the ~1.4M MiMC trace variables of a
 // batch.  All values are canonical little-endian 4 x u64.
+// Pinned by the reference's batch-58 batch-hash KAT (mimc.rs:386-450) and the
+// batch-70 Prover.toml roots, which tests/test_zbatch.py recomputes through
+// this code, and by equality with the Python restatement (same file).
 #include <stddef.h>
 #include <stdint.h>
 
