@@ -9,14 +9,20 @@ VariableBaseMSM::msm_bigint does 4x per Groth16 proof.
 
 Multi-GPU (torchrun, one process per GPU): weak scaling by point sharding.
 Every rank owns its own 2^log_n-point shard in HBM (the global MSM has
-N * 2^log_n terms); the exchange step is an RCCL all-gather of one affine
-partial point per rank + an exact group-law sum (zelana_amd/dist.py).
+N * 2^log_n terms); the exchange step is libzkmi's native all-gather of every
+rank's per-window bit sums (zkmi_msm_sharded_submit: ncclAllGather over xGMI
+when the backend is nccl) and the group-law sum in its epilogue.
 value = total point-scalar pairs processed by all ranks / max-over-ranks time.
+Config 5 (one global 2^26 MSM) is strong-scaled over the same communicator.
+Proofs (L2 scale and zelana_batch) and the NTT run as replicas at N > 1: every
+rank proves its own batches, as the forge swarm's chunk-per-worker model
+(forge/crates/prover-coordinator/src/dispatcher.rs:134,290).
 
 Inputs are synthetic (generated directly in HBM by libzkmi: P_i = k_i * G,
 uniform scalars) and resident before the timed region.  The CPU baseline is the
-oracle/ restatement of ark-ec's msm_bigint_wnaf run on this box's host cores on
-the same workload (rank 0, N=1 only), which also checks the GPU result.
+oracle/ restatement of arkworks run on this box's host cores (every core the
+process may use) on the same workloads -- MSM, NTT + INTT, one zelana_batch
+proof -- on rank 0 at N=1, each checked for equality with the GPU output.
 """
 from __future__ import annotations
 
@@ -46,7 +52,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-table", action="store_true", help="headline without the fixed-base table")
     ap.add_argument("--no-plain", action="store_true", help="skip the no-table side measurement")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: every usable core)")
+    ap.add_argument("--no-cpu-prove", action="store_true", help="skip the CPU baseline's zelana_batch proof leg")
     ap.add_argument("--no-ntt", action="store_true", help="skip the NTT 2^24 side measurement")
     ap.add_argument("--ntt-log-n", type=int, default=24)
     ap.add_argument("--no-l2", action="store_true", help="skip the L2 proof throughput side measurement")
@@ -86,6 +93,11 @@ def main():
     from zelana_amd.gpu import Context
 
     ctx = Context(gpu_index)
+    comm = None
+    if dist is not None:
+        from zelana_amd.dist import make_comm
+
+        comm = make_comm(ctx, backend)  # libzkmi's own communicator: RCCL, or host (gloo rehearsal)
     n = 1 << args.log_n
     bases = ctx.bases_generate(seed=1000 + rank, n=n)
     scalars = ctx.scalars_generate(seed=20 + rank, n=n)
@@ -99,19 +111,24 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    def finish(job):
-        part = ctx.msm_wait(job)
-        if dist is not None:
-            from zelana_amd.dist import combine_partials
+    finish = ctx.msm_wait
 
-            return combine_partials(part, _coll_dev)
-        return part
+    def submit(b, sc, cnt):
+        """one MSM: sharded over the communicator at N > 1 (collective)"""
+        return comm.msm_submit(b, sc, cnt) if comm is not None else ctx.msm_submit(b, sc, cnt)
+
+    def allmax(dt):
+        if dist is None:
+            return dt
+        t = torch.tensor([dt], dtype=torch.float64, device=_coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     ctx.set_lanes(args.lanes)
 
     def run(k):
         """k MSM steps, pipelined: args.lanes MSMs in flight, one per lane."""
-        return pipelined(lambda: ctx.msm_submit(bases, scalars, n), finish, k, args.depth or args.lanes)
+        return pipelined(lambda: submit(bases, scalars, n), finish, k, args.depth or args.lanes)
 
     def timed(k, warm, prof=False):
         """prof: HIP-event stage timers on (the stage breakdown comes from a
@@ -126,11 +143,7 @@ def main():
         sync_all()
         dt = time.perf_counter() - t0
         ctx.profile(False)
-        if dist is not None:
-            t = torch.tensor([dt], dtype=torch.float64, device=_coll_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        return res, dt
+        return res, allmax(dt)
 
     def stages(k):
         out = {}
@@ -186,21 +199,27 @@ def main():
 
     extra = {"msm_stage_ms_per_step": breakdown, "fixed_base_table": table, "msm_plain_no_table": plain,
              "lanes": args.lanes}
+    if comm is not None:
+        extra["msm_exchange"] = {"transport": ("rccl" if comm.info()[2] == 0 else "host:" + backend),
+                                 "what": "all-gather of every rank's per-window bit sums inside libzkmi "
+                                         "(zkmi_msm_sharded_submit), group-law sum in its epilogue"}
     # side measurements below: 2 lanes (the 2^26 MSM and the provers measured
     # best there: their MSMs are long enough that two overlap fully)
     ctx.set_lanes(2)
     if not args.no_big:
         extra["msm_global_2_%d" % args.big_log_n] = bench_msm_sharded(
-            ctx, args.big_log_n, args.big_steps, world, rank, dist, finish, sync_all, _coll_dev, 2)
-    if rank == 0 and world == 1 and not args.no_ntt:
-        extra["ntt"] = bench_ntt(ctx, args.ntt_log_n)
-    if rank == 0 and world == 1 and not args.no_l2:
-        extra["l2_proofs"] = bench_l2(ctx, args.l2_log_n, args.l2_steps)
-    if rank == 0 and world == 1 and not args.no_zbatch:
-        extra["zelana_batch_proofs"] = bench_zbatch(ctx, args.l2_steps)
+            ctx, args.big_log_n, args.big_steps, world, rank, submit, finish, sync_all, allmax, 2)
+    ntt_state = zb_state = None
+    if not args.no_ntt:
+        extra["ntt"], ntt_state = bench_ntt(ctx, args.ntt_log_n, world, sync_all, allmax)
+    if not args.no_l2:
+        extra["l2_proofs"] = bench_l2(ctx, args.l2_log_n, args.l2_steps, rank, world, sync_all, allmax)
+    if not args.no_zbatch:
+        extra["zelana_batch_proofs"], zb_state = bench_zbatch(ctx, args.l2_steps, world, sync_all, allmax)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(ctx, bases, scalars, n, result, args.cpu_threads)
+        cpu = cpu_baseline(ctx, bases, scalars, n, result, args.cpu_threads, ntt_state,
+                           None if args.no_cpu_prove else zb_state)
 
     pmc = pmc_record(kernel, args.log_n)
     traffic = pmc.get("hbm_bytes")
@@ -258,6 +277,9 @@ def main():
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        sync_all()
+        comm.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
@@ -278,44 +300,41 @@ def pipelined(submit, finish, k, depth):
     return res
 
 
-def bench_msm_sharded(ctx, log_total, steps, world, rank, dist, finish, sync_all, coll_dev, lanes=2):
+def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_all, allmax, lanes=2):
     """BASELINE.json configs[4]: ONE global BN254 G1 MSM of 2^log_total
     point-scalar pairs, point-sharded over the world's ranks (strong scaling:
     rank r owns elements [r*N/W, (r+1)*N/W) of the same global set, resident
-    with its fixed-base table), partials combined by an RCCL all-gather + exact
-    group-law sum.  The result is independent of the world size, so
-    result_sha256 must agree between the N=1/2/4/8 runs."""
+    with its fixed-base table), exchanged by libzkmi's communicator.  The
+    result is independent of the world size, so result_sha256 must agree
+    between the N=1/2/4/8 runs."""
     import hashlib
 
+    from zelana_amd.gpu import shard_range
+
     total = 1 << log_total
-    per = total // world
+    first, per = shard_range(total, world, rank)
     t0 = time.perf_counter()
-    bases = ctx.bases_generate(seed=1026, n=per, first=rank * per)
-    scalars = ctx.scalars_generate(seed=26, n=per, first=rank * per)
+    bases = ctx.bases_generate(seed=1026, n=per, first=first)
+    scalars = ctx.scalars_generate(seed=26, n=per, first=first)
     gen_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     info = bases.precompute()
     table_s = time.perf_counter() - t0
 
     def run(k):
-        return pipelined(lambda: ctx.msm_submit(bases, scalars, per), finish, k, lanes)
+        return pipelined(lambda: submit(bases, scalars, per), finish, k, lanes)
 
     run(1)
     sync_all()
     t0 = time.perf_counter()
     res = run(steps)
     sync_all()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = allmax(time.perf_counter() - t0)
     del bases, scalars
     return {
         "workload": f"BN254 G1 MSM 2^{log_total} (BASELINE.json configs[4]): one global MSM point-sharded over "
-                    f"{world} GPU(s), {per} resident points + fixed-base table per GPU; partials combined by all-gather + group-law sum",
+                    f"{world} GPU(s), {per} resident points + fixed-base table per GPU; bit sums exchanged by "
+                    "libzkmi's communicator, group-law sum in its epilogue",
         "value": round(total * steps / dt / 1e6, 2),
         "unit": "Mpoint-scalar/s",
         "ms_per_msm": round(dt / steps * 1e3, 3),
@@ -328,15 +347,22 @@ def bench_msm_sharded(ctx, log_total, steps, world, rank, dist, finish, sync_all
     }
 
 
-def bench_ntt(ctx, log_n, steps=5):
-    """Forward + inverse NTT of length 2^log_n on device data (configs[2])."""
-    from zelana_amd.gpu import DeviceBuffer
-
+def bench_ntt(ctx, log_n, world, sync_all, allmax, steps=5):
+    """Forward + inverse NTT of length 2^log_n on device data (configs[2]);
+    replicas at N > 1 (the transform does not shard).
+    Returns (line, state for the CPU leg: input and GPU forward output)."""
     n = 1 << log_n
     buf = ctx.scalars_generate(seed=24, n=n)
+    x0 = np.zeros((n, 4), np.uint64)
+    buf.download(x0)
     ctx.ntt_device(buf, log_n, False)
+    fwd = np.zeros((n, 4), np.uint64)
+    buf.download(fwd)  # the GPU forward transform of x0 (checked by the CPU leg)
     ctx.ntt_device(buf, log_n, True)
-    ctx.sync()
+    back = np.zeros((n, 4), np.uint64)
+    buf.download(back)
+    roundtrip = bool(np.array_equal(back, x0))
+    sync_all()
     ctx.profile(True)
     ctx.profile_reset()
     t0 = time.perf_counter()
@@ -344,34 +370,40 @@ def bench_ntt(ctx, log_n, steps=5):
         ctx.ntt_device(buf, log_n, False)
         ctx.ntt_device(buf, log_n, True)
     ctx.sync()
-    dt = (time.perf_counter() - t0) / steps
+    dt_local = (time.perf_counter() - t0) / steps
     ctx.profile(False)
-    tg, cg = ctx.profile_get("ntt_group")
+    sync_all()
+    dt = allmax(dt_local)
     stages = {}
     for k in ("ntt_group", "ntt_bitrev", "ntt_scale"):
         t, c = ctx.profile_get(k)
         if c:
             stages[k] = round(t / steps, 4)
     alg = NTT_BYTES_PER_ELEM * n * 2  # NTT + INTT
-    _ = DeviceBuffer
-    return {
-        "workload": f"Fr NTT + INTT 2^{log_n} (BASELINE.json configs[2]), natural order, device-resident",
+    line = {
+        "workload": f"Fr NTT + INTT 2^{log_n} (BASELINE.json configs[2]), natural order, device-resident"
+                    + (f"; {world} replicas (one transform pair per GPU)" if world > 1 else ""),
         "ms_per_ntt_intt": round(dt * 1e3, 4),
-        "melem_per_s": round(2 * n / dt / 1e6, 2),
-        "achieved_GBs": round(alg / dt / 1e9, 2),
-        "frac_hbm": round(alg / dt / 1e9 / HBM_PEAK_GBS, 5),
+        "melem_per_s": round(2 * n * world / dt / 1e6, 2),
+        "achieved_GBs": round(alg / dt_local / 1e9, 2),
+        "frac_hbm": round(alg / dt_local / 1e9 / HBM_PEAK_GBS, 5),
         "stage_ms": stages,
-        "note": "VALU-bound (8 x 2^23 x 3 Montgomery butterflies); algorithmic bytes = 64 B/elem/transform",
+        "roundtrip_exact": roundtrip,
+        "n_gpus": world,
+        "note": "VALU-bound (8 x 2^23 x 3 Montgomery butterflies); algorithmic bytes = 64 B/elem/transform; "
+                "achieved_GBs / frac_hbm per GPU",
     }
+    return line, {"log_n": log_n, "x": x0, "fwd": fwd}
 
 
-def bench_l2(ctx, log_n, steps):
+def bench_l2(ctx, log_n, steps, rank, world, sync_all, allmax):
     """Groth16 proofs/s at the config-4 scale (BASELINE.json configs[3]:
     ~2^22-constraint L2 block proof): synthetic R1CS of 2^log_n - 8 rows
     (3 terms per row in A and B, 1 in C; 8 instance variables = One + 7
     public inputs; one witness per row), random proving key of that shape
     generated in HBM, witness resident in HBM.  One step = witness map
-    (3 mat-vecs, 7 NTTs) + 4 G1 MSMs + 1 G2 MSM + assembly."""
+    (3 mat-vecs, 7 NTTs) + 4 G1 MSMs + 1 G2 MSM + assembly.  At N > 1 every
+    rank proves its own batches (replicas)."""
     from zelana_amd import gpu
     from zelana_amd.r1cs import synthetic_fast
 
@@ -379,8 +411,8 @@ def bench_l2(ctx, log_n, steps):
     m = (1 << log_n) - l
     w = m
     t0 = time.perf_counter()
-    cs, z = synthetic_fast(m, l, w, seed=70)
-    pk = gpu.synthetic_pk(ctx, 70, log_n, l, w)
+    cs, z = synthetic_fast(m, l, w, seed=70 + rank)
+    pk = gpu.synthetic_pk(ctx, 70 + rank, log_n, l, w)
     dev = gpu.R1CSDevice(ctx, cs)
     dz = gpu.DeviceBuffer(ctx, z.nbytes)
     dz.upload(z)
@@ -389,6 +421,7 @@ def bench_l2(ctx, log_n, steps):
     def timed():
         gpu.groth16_prove_resident(ctx, pk, dev, dz, 12345, 67890)
         ctx.sync()
+        sync_all()
         ctx.profile(True)
         ctx.profile_reset()
         t0 = time.perf_counter()
@@ -396,8 +429,10 @@ def bench_l2(ctx, log_n, steps):
         for i in range(steps):
             outs.append(gpu.groth16_prove_resident(ctx, pk, dev, dz, 12345 + i, 67890 + i))
         ctx.sync()
-        dt = (time.perf_counter() - t0) / steps
+        dt_local = (time.perf_counter() - t0) / steps
         ctx.profile(False)
+        sync_all()
+        dt = allmax(dt_local)
         st = {}
         for k in ("g16_matvec", "g16_scale", "g16_qap", "ntt_group", "ntt_small", "msm_sort", "msm_items_plan", "msm_acc0_g1",
                   "msm_acc0_g2", "msm_accN", "msm_bucket_reduce", "msm_host_epilogue"):
@@ -416,25 +451,32 @@ def bench_l2(ctx, log_n, steps):
     del dev, pk
     return {
         "workload": f"Groth16 prove, domain 2^{log_n}: {m} constraints, {l} instance + {w} witness vars, {nnz} non-zeros "
-                    "(BASELINE.json configs[3] scale; synthetic R1CS + random pk generated in HBM)",
-        "proofs_per_s": round(1.0 / dt, 3),
+                    "(BASELINE.json configs[3] scale; synthetic R1CS + random pk generated in HBM; the reference's "
+                    "own L2BlockCircuit R1CS is parity-unpinned: no reference fixture covers it)"
+                    + (f"; {world} replicas, one per GPU" if world > 1 else ""),
+        "proofs_per_s": round(world / dt, 3),
+        "proofs_per_s_per_gpu": round(1.0 / dt, 3),
         "ms_per_proof": round(dt * 1e3, 2),
+        "n_gpus": world,
         "stage_ms_per_proof": stages,
         "fixed_base_tables": {"build_s": round(table_s, 2), "same_proofs_as_plain": same},
-        "plain_no_table": {"proofs_per_s": round(1.0 / plain_dt, 3), "ms_per_proof": round(plain_dt * 1e3, 2),
+        "plain_no_table": {"proofs_per_s": round(world / plain_dt, 3), "ms_per_proof": round(plain_dt * 1e3, 2),
                            "stage_ms_per_proof": plain_st},
         "setup_s": round(setup_s, 1),
         "note": "witness z resident in HBM; uploading it costs z_bytes/PCIe extra (see DESIGN.md)",
     }
 
 
-def bench_zbatch(ctx, steps):
+def bench_zbatch(ctx, steps, world, sync_all, allmax):
     """Groth16 proofs/s on the config-4 circuit itself: forge/circuits/
     zelana_batch (MiMC Merkle batch) arithmetized by zelana_amd/zbatch.py and
     filled from its Prover.toml (batch 70: 5 transfers; committed fixture).
     Proving key: a REAL key, Groth16::circuit_specific_setup with StdRng(0) as
     keygen.rs does, built on the GPU (zkmi_groth16_setup; the same proof
-    verifies under its VK in tests/test_gpu_keygen.py)."""
+    verifies under its VK in tests/test_gpu_keygen.py).  Two rates:
+    resident (z already in HBM) and end to end per batch (witness generation
+    + upload of z + prove, what Groth16Prover::prove does after synthesis).
+    Replicas at N > 1.  Returns (line, state for the CPU prove leg)."""
     from zelana_amd import gpu, zbatch
     from zelana_amd.keygen import circuit_specific_setup
     from zelana_amd.rng import StdRng
@@ -443,10 +485,6 @@ def bench_zbatch(ctx, steps):
     d = zbatch.load_prover_toml(os.path.join(ROOT, "tests", "golden", "zelana_batch_70_Prover.toml"))
     cs, z, _ = zbatch.build(d)
     synth_s = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    _, zw, _ = zbatch.build(d, witness_only=True)  # per batch: the R1CS and key are fixed
-    witness_s = time.perf_counter() - t0
-    assert np.array_equal(zw, z)
     log_n = 0
     while (1 << log_n) < cs.num_constraints + cs.num_instance:
         log_n += 1
@@ -463,33 +501,100 @@ def bench_zbatch(ctx, steps):
     setup_s = time.perf_counter() - t0
     rng = StdRng.seed_from_u64(int(d["batch_id"]))
     r, s = rng.fr_rand(), rng.fr_rand()
-    gpu.groth16_prove_resident(ctx, pk, dev, dz, r, s)
+    proof = gpu.groth16_prove_resident(ctx, pk, dev, dz, r, s)
     ctx.sync()
+    sync_all()
     t0 = time.perf_counter()
     for _ in range(steps):
         gpu.groth16_prove_resident(ctx, pk, dev, dz, r, s)
     ctx.sync()
-    dt = (time.perf_counter() - t0) / steps
+    dt_local = (time.perf_counter() - t0) / steps
+    sync_all()
+    dt = allmax(dt_local)
+    # end to end per batch: witness (host), H2D of z, prove
+    sync_all()
+    t0 = time.perf_counter()
+    wit = 0.0
+    for _ in range(steps):
+        t1 = time.perf_counter()
+        _, zw, _ = zbatch.build(d, witness_only=True)
+        wit += time.perf_counter() - t1
+        dz.upload(zw)
+        gpu.groth16_prove_resident(ctx, pk, dev, dz, r, s)
+    ctx.sync()
+    e2e_local = (time.perf_counter() - t0) / steps
+    sync_all()
+    e2e = allmax(e2e_local)
+    same_z = bool(np.array_equal(zw, z))
     del dev, pk
-    return {
+    line = {
         "workload": f"zelana_batch batch 70 (forge/circuits/zelana_batch, Prover.toml): {cs.num_constraints} "
-                    f"constraints, {cs.num_variables} variables, domain 2^{log_n}; r, s from StdRng(batch_id)",
-        "proofs_per_s": round(1.0 / dt, 3),
+                    f"constraints, {cs.num_variables} variables, domain 2^{log_n}; r, s from StdRng(batch_id)"
+                    + (f"; {world} replicas, one per GPU" if world > 1 else ""),
+        "proofs_per_s": round(world / dt, 3),
+        "proofs_per_s_per_gpu": round(1.0 / dt, 3),
         "ms_per_proof": round(dt * 1e3, 2),
+        "n_gpus": world,
+        "end_to_end": {"proofs_per_s": round(world / e2e, 3), "ms_per_batch": round(e2e * 1e3, 2),
+                       "witness_ms_per_batch": round(wit / steps * 1e3, 2), "witness_equal": same_z,
+                       "what": "per batch: witness generation + H2D of z + prove (z not resident)"},
         "r1cs_and_witness_synthesis_s_host": round(synth_s, 2),
-        "witness_s_per_batch_host": round(witness_s, 3),
         "witness_native_mimc": zbatch._native_mimc() is not None,
         "keygen_s_gpu": round(keygen_s, 3),
         "table_and_upload_s": round(setup_s, 2),
-        "note": "real proving key (GPU circuit_specific_setup, StdRng(0) as keygen.rs); witness resident in HBM",
+        "note": "real proving key (GPU circuit_specific_setup, StdRng(0) as keygen.rs); proofs_per_s with the "
+                "witness resident in HBM",
     }
+    return line, {"cs": cs, "z": z, "r": r, "s": s, "proof": proof}
 
 
-def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads):
-    """oracle/ port of ark-ec msm_bigint_wnaf on the same inputs, host cores."""
+def host_cores():
+    """Cores this process may use: the affinity mask, capped by a cgroup CPU
+    quota (the GPU box grants each job a share of a large host), plus the
+    CPU model, for the cpu_baseline record."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, {"host_cpus": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "cpu_model": model}
+
+
+def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb_state=None):
+    """oracle/ restatement of arkworks on this box's host cores, same inputs
+    as the GPU legs, each leg checked for equality with the GPU output:
+      msm   ark-ec msm_bigint_wnaf on the headline's 2^20 bases / scalars
+      ntt   ark-poly radix-2 forward + inverse at 2^24 (configs[2])
+      prove ark-groth16 prove of zelana_batch batch 70 (configs[3]) under the
+            oracle's own StdRng(0) key (setup untimed), same r and s."""
+    import ctypes
+
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ctypes as O  # test infrastructure: the checker / CPU baseline only
 
+    cores, hw = host_cores()
+    threads = threads or cores
     pts = bases.export()
     sc = np.zeros((n, 4), np.uint64)
     scalars.download(sc)
@@ -503,15 +608,55 @@ def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads):
         dt += time.perf_counter() - t1
         reps += 1
     per = dt / reps
-    return {
+    out = {
         "value": round(n / per / 1e6, 3),
         "unit": "Mpoint-scalar/s",
         "cores": threads,
         "kind": "port",
         "sample": f"full 2^{int(np.log2(n))} workload of the timed step (same bases/scalars), {reps} rep(s), "
-                  f"{per*1e3:.1f} ms each; pthreads over windows like ark-ec's rayon",
+                  f"{per*1e3:.1f} ms each; pthreads over windows x point chunks (every core busy)",
         "gpu_matches_cpu": bool(np.array_equal(gpu_result, want)),
+        "hardware": hw,
+        "legs": {},
     }
+    if ntt_state is not None:
+        log_n, x, fwd = ntt_state["log_n"], ntt_state["x"], ntt_state["fwd"]
+        t0 = time.perf_counter()
+        cf = O.ntt(x, log_n, False, False, threads=threads)
+        t1 = time.perf_counter()
+        ci = O.ntt(cf, log_n, True, False, threads=threads)
+        t2 = time.perf_counter()
+        out["legs"]["ntt"] = {
+            "value": round(2 * (1 << log_n) / (t2 - t0) / 1e6, 2), "unit": "Melem/s (NTT + INTT)",
+            "ms_per_ntt_intt": round((t2 - t0) * 1e3, 1), "cores": threads, "kind": "port",
+            "sample": f"one forward + one inverse transform of the 2^{log_n} bench vector",
+            "gpu_matches_cpu": bool(np.array_equal(cf.reshape(-1, 4), fwd) and np.array_equal(ci.reshape(-1, 4), x)),
+        }
+    if zb_state is not None:
+        cs, z, r, s = zb_state["cs"], zb_state["z"], zb_state["r"], zb_state["s"]
+        st, keep = O.make_r1cs(cs)
+        rng = O.Rng(0)
+        t0 = time.perf_counter()
+        opk = O.lib().oracle_groth16_setup(ctypes.byref(st), rng.h, threads)
+        setup_s = time.perf_counter() - t0
+        a, b, c = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+        rs = np.concatenate([O.int_to_limbs(r), O.int_to_limbs(s)])
+        t0 = time.perf_counter()
+        rc = O.lib().oracle_groth16_prove(opk, ctypes.byref(st), O.P(np.ascontiguousarray(z)), None, O.P(rs), threads,
+                                          O.P(a), O.P(b), O.P(c), None)
+        dtp = time.perf_counter() - t0
+        O.lib().oracle_pk_free(opk)
+        ga, gb, gc = zb_state["proof"]
+        out["legs"]["prove"] = {
+            "value": round(1.0 / dtp, 4), "unit": "proofs/s", "s_per_proof": round(dtp, 2), "cores": threads,
+            "kind": "port",
+            "sample": "one Groth16 proof of zelana_batch batch 70 (2^21 domain) with the oracle's StdRng(0) key "
+                      f"(its setup, {setup_s:.1f} s, untimed), r and s from StdRng(70)",
+            "gpu_matches_cpu": bool(rc == 0 and np.array_equal(a, ga) and np.array_equal(b, gb)
+                                    and np.array_equal(c, gc)),
+        }
+        del keep
+    return out
 
 
 def pmc_record(kernel, log_n):

@@ -136,10 +136,52 @@ int zkmi_msm_set_window(zkmi_ctx* ctx, int c);
  * consecutive submissions so their latency-bound tails overlap; 1..8. */
 int zkmi_msm_set_lanes(zkmi_ctx* ctx, int lanes);
 
-/* canonical affine point arithmetic helpers (host; used to combine per-GPU
- * partial MSM results after an RCCL all-gather) */
+/* canonical affine point arithmetic helpers (host) */
 int zkmi_g1_add(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
 int zkmi_g2_add(const uint64_t a[16], const uint64_t b[16], uint64_t out[16]);
+
+/* ------------------------------------------------------------- multi-GPU
+ * MSM point sharding (BASELINE.json configs[4]): one rank per
+ * GPU (one process per GPU, or one host thread per GPU in one process), each
+ * holding its own zkmi_ctx and the shard [first, first + count) of the bases
+ * resident in its HBM (zkmi_shard_range + zkmi_bases_create_*).  A sharded MSM
+ * runs the full Pippenger pipeline on every shard, then exchanges the
+ * per-window bit sums (the partially reduced buckets, ~c x W XYZZ points per
+ * rank) with ONE all-gather and sums them across ranks in the group-law
+ * epilogue: the "all-reduce of partial bucket sums" (RCCL has no elliptic-
+ * curve reduction operator).  Every rank returns the global sum.
+ *
+ * Transports:
+ *   zkmi_comm_init       RCCL (ncclAllGather over xGMI), enqueued on the MSM
+ *                        lane's stream: no host round trip in the exchange.
+ *                        The ranks' unique id comes from zkmi_comm_unique_id
+ *                        on one rank, broadcast by the host (like NCCL).
+ *   zkmi_comm_init_host  the host supplies the all-gather (MPI, a TCP store,
+ *                        pipes ...): for hosts without RCCL, or ranks that share
+ *                        one GPU (RCCL refuses two ranks on one device).
+ * Collectives must be issued in the same order on every rank.  Ranks' window
+ * plans must agree (equal shard sizes and the same zkmi_bases_precompute
+ * choice); a mismatch is detected and reported as ZKMI_EINVAL on every rank. */
+typedef struct zkmi_comm zkmi_comm;
+#define ZKMI_COMM_ID_BYTES 128
+/* all-gather of `bytes` from every rank: recv = rank 0's bytes || rank 1's ... */
+typedef int (*zkmi_allgather_fn)(void* user, const void* send, void* recv, size_t bytes);
+int zkmi_comm_unique_id(uint8_t id[ZKMI_COMM_ID_BYTES]);
+int zkmi_comm_init(zkmi_ctx* ctx, const uint8_t id[ZKMI_COMM_ID_BYTES], int nranks, int rank, zkmi_comm** out);
+int zkmi_comm_init_host(zkmi_ctx* ctx, int nranks, int rank, zkmi_allgather_fn allgather, void* user,
+                        zkmi_comm** out);
+void zkmi_comm_destroy(zkmi_comm* comm);
+/* [nranks, rank, transport (0 = RCCL, 1 = host)] */
+int zkmi_comm_info(const zkmi_comm* comm, int out[3]);
+/* contiguous point shard of rank `rank`: the first total % nranks ranks get
+ * one extra point */
+int zkmi_shard_range(size_t total, int nranks, int rank, size_t* first, size_t* count);
+/* sum over ALL ranks of sum_{i<n} scalars[i] * shard[offset + i]; collective.
+ * Scalars are this rank's slice (device memory, n x 32 B canonical). */
+int zkmi_msm_sharded_submit(zkmi_comm* comm, const zkmi_bases* shard, size_t offset, const void* d_scalars,
+                            size_t n, zkmi_msm_job** job);
+int zkmi_msm_sharded(zkmi_comm* comm, const zkmi_bases* shard, size_t offset, const void* d_scalars, size_t n,
+                     uint64_t* out_affine);
 
 /* ------------------------------------------------------------- NTT */
 /* In-place radix-2 transform over Fr of length 2^log_n, natural order in and

@@ -5,6 +5,10 @@
  * else ln_without_floats(n) + 2 with ln_without_floats(n) = ceil_log2(n)*69/100,
  * 2^(c-1)... buckets per window, window sums in parallel (rayon over windows ->
  * pthreads over windows here), windows combined high-to-low by c doublings.
+ * When the host has more threads than windows, each window is also cut into
+ * point chunks (work item = window x chunk, chunk partials summed per window)
+ * so every core works: the sum is the same group element, the CPU baseline
+ * gets every core (bench.py), and no output changes.
  * Bases/scalars zip-truncate to the shorter input, as in arkworks.
  * Test infrastructure + timed CPU baseline ("port") only.
  */
@@ -42,9 +46,26 @@ static void make_digits(const uint64_t s[4], int w, int num_bits, int32_t* out) 
   }
 }
 
+/* chunks per window: minimises (rounds of work items) x (item time) with
+ * item time ~ points per chunk + ~3 additions per bucket for its running sum */
+static int msm_chunks(size_t n, int c, int count, int nthreads) {
+  int best = 1;
+  double best_t = 1e300;
+  for (int k = 1; k <= 64; k++) {
+    if ((size_t)k * 1024 > n && k > 1) break;
+    double rounds = (double)(((size_t)count * k + nthreads - 1) / nthreads);
+    double t = rounds * ((double)n / k + 3.0 * (double)((size_t)1 << c));
+    if (t < best_t * 0.98) {
+      best_t = t;
+      best = k;
+    }
+  }
+  return best;
+}
+
 #define DEFINE_MSM(P, J, A, T, NEG)                                                         \
   typedef struct {                                                                          \
-    const A* bases; const int32_t* digits; size_t n; int c, count, next;                    \
+    const A* bases; const int32_t* digits; size_t n; int c, count, next, nch;               \
     pthread_mutex_t* mu; J* sums;                                                           \
   } P##_msm_job;                                                                            \
   static void* P##_msm_worker(void* arg) {                                                  \
@@ -53,11 +74,13 @@ static void make_digits(const uint64_t s[4], int w, int num_bits, int32_t* out) 
     J* buckets = (J*)malloc(nb * sizeof(J));                                                \
     for (;;) {                                                                              \
       pthread_mutex_lock(jb->mu);                                                           \
-      int w = jb->next++;                                                                   \
+      int item = jb->next++;                                                                \
       pthread_mutex_unlock(jb->mu);                                                         \
-      if (w >= jb->count) break;                                                            \
+      if (item >= jb->count * jb->nch) break;                                               \
+      int w = item / jb->nch, ch = item % jb->nch;                                          \
+      size_t lo = jb->n * ch / jb->nch, hi = jb->n * (ch + 1) / jb->nch;                    \
       for (size_t b = 0; b < nb; b++) P##_set_inf(&buckets[b]);                             \
-      for (size_t i = 0; i < jb->n; i++) {                                                  \
+      for (size_t i = lo; i < hi; i++) {                                                    \
         int32_t d = jb->digits[i * jb->count + w];                                          \
         if (d > 0) P##_add_mixed(&buckets[d - 1], &buckets[d - 1], &jb->bases[i]);          \
         else if (d < 0) {                                                                   \
@@ -69,7 +92,7 @@ static void make_digits(const uint64_t s[4], int w, int num_bits, int32_t* out) 
       J run, res;                                                                           \
       P##_set_inf(&run); P##_set_inf(&res);                                                 \
       for (size_t b = nb; b-- > 0;) { P##_add(&run, &run, &buckets[b]); P##_add(&res, &res, &run); } \
-      jb->sums[w] = res;                                                                    \
+      jb->sums[item] = res;                                                                 \
     }                                                                                       \
     free(buckets);                                                                          \
     return NULL;                                                                            \
@@ -92,11 +115,15 @@ static void make_digits(const uint64_t s[4], int w, int num_bits, int32_t* out) 
       pthread_create(&th[t], NULL, P##_dig_worker, &dj[t]);                                 \
     }                                                                                       \
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);                           \
-    J* sums = (J*)malloc(count * sizeof(J));                                                \
+    int nch = msm_chunks(n, c, count, nthreads);                                            \
+    J* sums = (J*)malloc((size_t)count * nch * sizeof(J));                                  \
     pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;                                         \
-    P##_msm_job job = {bases, digits, n, c, count, 0, &mu, sums};                           \
+    P##_msm_job job = {bases, digits, n, c, count, 0, nch, &mu, sums};                      \
     for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, P##_msm_worker, &job);  \
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);                           \
+    for (int w = 0; w < count; w++)                                                         \
+      for (int k = 1; k < nch; k++) P##_add(&sums[w * nch], &sums[w * nch], &sums[w * nch + k]); \
+    for (int w = 1; w < count; w++) sums[w] = sums[w * nch];                                \
     J total;                                                                                \
     P##_set_inf(&total);                                                                    \
     for (int w = count - 1; w >= 1; w--) {                                                  \

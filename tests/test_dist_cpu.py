@@ -1,7 +1,8 @@
-"""N>1 path on CPU: world_size-2 gloo processes combine per-rank partial MSMs
-(all-gather + exact group-law sum) and must equal the MSM of the
-concatenated shards.  Partial MSMs come from the oracle (no GPU here); the
-combine code is the product's (zelana_amd.dist + libzkmi host point add)."""
+"""N>1 path on CPU (gloo, no GPU here): the host-side pieces of the sharded
+MSM -- the torch.distributed all-gather that drives libzkmi's host transport,
+zkmi_shard_range, and the group-law combine of per-rank partials (partial
+MSMs from the oracle) -- must equal the single-rank results.  The GPU side
+of the exchange is tests/test_gpu_multi.py."""
 import os
 import sys
 
@@ -28,6 +29,49 @@ def _worker(rank, world, port, q):
     q.put((rank, tot.tolist()))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _ag_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from zelana_amd.dist import torch_allgather
+    from zelana_amd.gpu import shard_range
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ag = torch_allgather()
+    parts = ag(bytes([rank + 1]) * 40)  # the zkmi host-transport callback's contract
+    first, cnt = shard_range(1000003, world, rank)
+    q.put((rank, [p.hex() for p in parts], first, cnt))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_host_transport_allgather_and_shards():
+    """The torch.distributed all-gather that feeds libzkmi's host transport
+    (zkmi_comm_init_host) returns every rank's bytes in rank order, and
+    zkmi_shard_range tiles [0, total) with contiguous shards."""
+    from zelana_amd._lib import LIB_PATH
+    if not os.path.exists(LIB_PATH):
+        pytest.skip("libzkmi.so not built")
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_ag_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [(bytes([r + 1]) * 40).hex() for r in range(world)]
+    nxt = 0
+    for rank, parts, first, cnt in res:
+        assert parts == want
+        assert first == nxt
+        nxt += cnt
+    assert nxt == 1000003
+    assert max(c for *_, c in res) - min(c for *_, c in res) <= 1
 
 
 def test_two_rank_combine():

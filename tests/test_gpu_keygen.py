@@ -109,20 +109,40 @@ def test_synthetic_keygen_matches_oracle(ctx, m, l, w, seed):
     O.lib().oracle_pk_free(opk)
 
 
+def _threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
 def test_zbatch_full_keygen_prove_verify(ctx):
-    """Config 4 with a real key: batch 70 of forge/circuits/zelana_batch
-    (Prover.toml), GPU keygen (seed 0), GPU proof with r, s from
-    StdRng(batch_id), pairing check against the key's VK."""
+    """Config 4 with a real key, at full size: batch 70 of
+    forge/circuits/zelana_batch (Prover.toml, 1.42M constraints, 2^21 domain).
+    GPU keygen (seed 0) serializes to the oracle's key bytes; the GPU proof
+    with r, s from StdRng(batch_id) is byte-identical to the oracle's proof
+    under the oracle's key (configs[3]: "bit-exact vs CPU"); and it passes the
+    pairing check against the key's VK."""
     import pairing as PR
     from zelana_amd import gpu, zbatch
     from zelana_amd.rng import StdRng
     d = zbatch.load_prover_toml(os.path.join(GOLD, "zelana_batch_70_Prover.toml"))
     cs, z, _ = zbatch.build(d)
     pk, vk = _gpu_key(ctx, cs, 0)
+    st, keep = O.make_r1cs(cs)
+    opk = O.lib().oracle_groth16_setup(ctypes.byref(st), O.Rng(0).h, _threads())
+    size = O.lib().oracle_pk_serialize(opk, 1, None, 0)
+    obytes = np.zeros(size, np.uint8)
+    O.lib().oracle_pk_serialize(opk, 1, obytes.ctypes.data, size)
+    assert pk.serialize() == obytes.tobytes(), "GPU keygen != oracle keygen at full size"
     pk.precompute()
     rng = StdRng.seed_from_u64(int(d["batch_id"]))
     r, s = rng.fr_rand(), rng.fr_rand()
     a, b, c = gpu.groth16_prove(ctx, pk, cs, z, r, s)
+    oa, ob, oc = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+    rs = np.concatenate([O.int_to_limbs(r), O.int_to_limbs(s)])
+    assert O.lib().oracle_groth16_prove(opk, ctypes.byref(st), O.P(z), None, O.P(rs), _threads(),
+                                        O.P(oa), O.P(ob), O.P(oc), None) == 0
+    O.lib().oracle_pk_free(opk)
+    assert np.array_equal(a, oa) and np.array_equal(b, ob) and np.array_equal(c, oc), "GPU proof != oracle proof"
+    assert gpu.proof_to_solana_bytes(a, b, c) == gpu.proof_to_solana_bytes(oa, ob, oc)
     pub = [O.limbs_to_int(z[i]) for i in range(1, cs.num_instance)]
     vkd = _vk_points(vk, cs.num_instance)
     g1_add, g1_mul = PR.oracle_g1_ops()

@@ -1,0 +1,177 @@
+"""GPU: point-sharded MSM through the C ABI's communicator (zkmi.h multi-GPU
+section; SURVEY.md §8e, BASELINE.json configs[4]).
+
+* the C++ host test (tests/host/test_sharded_msm.cpp) forks two ranks that
+  drive a sharded MSM through zkmi.h alone, here over the host transport (a
+  1-GPU box: both ranks share the card; RCCL refuses two ranks on one device);
+* the RCCL transport with a one-rank communicator (the enqueue / event /
+  all-gather / epilogue path; the N-rank exchange itself is RCCL's);
+* two ranks in one process (one host thread per rank, as a Rust host with one
+  thread per GPU would run them) over the host transport from Python;
+* the context device guard: a context driven from another thread.
+
+Every sharded result must equal the one-rank MSM over the whole set."""
+import os
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from zelana_amd.gpu import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _global(ctx, pseed, sseed, total):
+    b = ctx.bases_generate(seed=pseed, n=total)
+    s = ctx.scalars_generate(seed=sseed, n=total)
+    return ctx.msm(b, s)
+
+
+def test_cpp_two_rank_sharded_msm():
+    exe = os.path.join(ROOT, "zelana_amd", "test_sharded_msm")
+    assert os.path.exists(exe), "build first (python -m zelana_amd.build_native)"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "host transport: rank0 PASS, rank1 PASS" in r.stdout
+
+
+def test_rccl_one_rank_comm(ctx):
+    from zelana_amd import gpu
+    comm = gpu.Comm.rccl(ctx, gpu.comm_unique_id(), 1, 0)
+    assert comm.info() == (1, 0, 0)
+    total = (1 << 16) + 5
+    b = ctx.bases_generate(seed=77, n=total)
+    s = ctx.scalars_generate(seed=78, n=total)
+    want = ctx.msm(b, s)
+    assert np.array_equal(comm.msm(b, s, total), want)
+    # pipelined submissions on several lanes stay in order through the comm stream
+    ctx.set_lanes(3)
+    jobs = [comm.msm_submit(b, s, total) for _ in range(4)]
+    for j in jobs:
+        assert np.array_equal(ctx.msm_wait(j), want)
+    b.precompute()
+    assert np.array_equal(comm.msm(b, s, total), want)
+    ctx.set_lanes(2)
+    comm.close()
+
+
+def _thread_allgather(nranks):
+    """In-process all-gather for rank threads (host transport)."""
+    lock = threading.Condition()
+    state = {"gen": 0, "parts": {}, "done": {}}
+
+    def make(rank):
+        def ag(blob: bytes):
+            with lock:
+                gen = state["gen"]
+                state["parts"][rank] = blob
+                if len(state["parts"]) == nranks:
+                    state["done"][gen] = [state["parts"][r] for r in range(nranks)]
+                    state["parts"] = {}
+                    state["gen"] += 1
+                    lock.notify_all()
+                else:
+                    assert lock.wait_for(lambda: gen in state["done"], timeout=60)
+                return state["done"][gen]
+        return ag
+    return make
+
+
+def test_two_rank_threads_host_transport(ctx):
+    from zelana_amd import gpu
+    nr = 2
+    make = _thread_allgather(nr)
+    total = 3 * (1 << 15) + 1
+    want = _global(ctx, 1026, 26, total)
+    results, errors = [None] * nr, []
+
+    def rank_main(r):
+        try:
+            c = gpu.Context(0)
+            comm = gpu.Comm.host(c, nr, r, make(r))
+            first, cnt = gpu.shard_range(total, nr, r)
+            b = c.bases_generate(seed=1026, n=cnt, first=first)
+            s = c.scalars_generate(seed=26, n=cnt, first=first)
+            results[r] = comm.msm(b, s, cnt)
+            del b, s
+            comm.close()
+            c.close()
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(nr)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not errors, errors
+    for r in range(nr):
+        assert np.array_equal(results[r], want)
+
+
+def test_context_from_another_thread(ctx):
+    """A context created here and driven from a worker thread (the device
+    guard selects the context's device on entry, INTEGRATION.md's tokio
+    blocking-pool threads)."""
+    b = ctx.bases_generate(seed=5, n=4096)
+    s = ctx.scalars_generate(seed=6, n=4096)
+    want = ctx.msm(b, s)
+    out = {}
+    t = threading.Thread(target=lambda: out.setdefault("r", ctx.msm(b, s)))
+    t.start()
+    t.join(timeout=60)
+    assert np.array_equal(out["r"], want)
+
+
+def test_config5_2pow26_eight_shards_native_exchange(ctx):
+    """Config 5's exact decomposition at its size on one GPU: 8 rank threads,
+    each with its own context, shard [r 2^23, (r+1) 2^23) of the global 2^26
+    set and its own fixed-base table, run the sharded MSM through the native
+    communicator (host transport); every rank's result equals the one-GPU
+    2^26 MSM with the c = 22 / 12-copy table."""
+    from zelana_amd import gpu
+    nr, log_total = 8, 26
+    total = 1 << log_total
+    big = ctx.bases_generate(seed=1026, n=total)
+    info = big.precompute()
+    assert info[1:] == (22, 12, 1), info
+    sc = ctx.scalars_generate(seed=26, n=total)
+    want = ctx.msm(big, sc)
+    del big, sc
+    make = _thread_allgather(nr)
+    results, errors = [None] * nr, []
+
+    def rank_main(r):
+        try:
+            c = gpu.Context(0)
+            comm = gpu.Comm.host(c, nr, r, make(r))
+            first, cnt = gpu.shard_range(total, nr, r)
+            b = c.bases_generate(seed=1026, n=cnt, first=first)
+            b.precompute()
+            s = c.scalars_generate(seed=26, n=cnt, first=first)
+            results[r] = comm.msm(b, s, cnt)
+            del b, s
+            comm.close()
+            c.close()
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(nr)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errors, errors
+    for r in range(nr):
+        assert np.array_equal(results[r], want), r

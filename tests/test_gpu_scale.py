@@ -7,8 +7,9 @@ do not need the CPU oracle to redo the whole job:
   (sum_j a_j omega^{jk}, omega = 5^((r-1)/2^28) ^ (2^28 / n), coset:
   a_j -> a_j g^j) — the arkworks Radix2EvaluationDomain definition.
 * G1 MSM at 2^24 with the fixed-base table (configs[4]'s per-GPU scale at
-  N=4): linearity MSM(a) + MSM(b) = MSM(a + b); and a sparse-scalar MSM
-  equal to the oracle's sum over its non-zero terms.
+  N=4) and at 2^26 (configs[4]'s global size, c = 22 / 12-copy table):
+  linearity MSM(a) + MSM(b) = MSM(a + b); and a sparse-scalar MSM equal to
+  the oracle's sum over its non-zero terms.
 """
 import numpy as np
 import pytest
@@ -124,11 +125,14 @@ def test_ntt_2pow24_sparse_exact(ctx, inverse, coset):
         assert to_int(out[k]) == acc, (k, inverse, coset)
 
 
-def test_msm_2pow24_table_linearity_and_sparse(ctx):
+@pytest.mark.parametrize("log_n", [24, 26])
+def test_msm_table_linearity_and_sparse(ctx, log_n):
     from zelana_amd.gpu import DeviceBuffer, g1_add
-    n = 1 << 24
-    bases = ctx.bases_generate(seed=1024, n=n)
-    bases.precompute()
+    n = 1 << log_n
+    bases = ctx.bases_generate(seed=1000 + log_n, n=n)
+    info = bases.precompute()
+    if log_n == 26:
+        assert info[1:] == (22, 12, 1), info  # the config-5 plan
     a = ctx.scalars_generate(seed=31, n=n)
     b = ctx.scalars_generate(seed=32, n=n)
     ha, hb = np.zeros((n, 4), np.uint64), np.zeros((n, 4), np.uint64)
@@ -138,7 +142,7 @@ def test_msm_2pow24_table_linearity_and_sparse(ctx):
     s.upload(add_mod_r(ha, hb))
     ma, mb, ms = ctx.msm(bases, a), ctx.msm(bases, b), ctx.msm(bases, s)
     assert np.array_equal(g1_add(ma, mb), ms)
-    # sparse scalars: the full 2^24 run against the oracle over its non-zero terms
+    # sparse scalars: the full-size run against the oracle over its non-zero terms
     rng = np.random.default_rng(7)
     idx = np.sort(rng.choice(n, 300, replace=False))
     sp = np.zeros((n, 4), np.uint64)
@@ -148,3 +152,7 @@ def test_msm_2pow24_table_linearity_and_sparse(ctx):
     got = ctx.msm(bases, d)
     pts = bases.export()[idx]
     assert np.array_equal(got, O.msm_g1(np.ascontiguousarray(pts), np.ascontiguousarray(ha[idx])))
+    # and the same sparse MSM with the table's window pinned off (plain Pippenger)
+    ctx.set_window(16)
+    assert np.array_equal(ctx.msm(bases, d), got)
+    ctx.set_window(0)

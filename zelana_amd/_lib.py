@@ -68,6 +68,14 @@ SIGNATURES = [
     ("zkmi_msm_set_window", ctypes.c_int, [vp, ctypes.c_int]),
     ("zkmi_msm_set_lanes", ctypes.c_int, [vp, ctypes.c_int]),
     ("zkmi_msm_submit_shared", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_int, sz, vp, sz, ctypes.POINTER(vp)]),
+    ("zkmi_comm_unique_id", ctypes.c_int, [u8p]),
+    ("zkmi_comm_init", ctypes.c_int, [vp, u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),
+    ("zkmi_comm_init_host", ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.POINTER(vp)]),
+    ("zkmi_comm_destroy", None, [vp]),
+    ("zkmi_comm_info", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
+    ("zkmi_shard_range", ctypes.c_int, [sz, ctypes.c_int, ctypes.c_int, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
+    ("zkmi_msm_sharded_submit", ctypes.c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp)]),
+    ("zkmi_msm_sharded", ctypes.c_int, [vp, vp, sz, vp, sz, u64p]),
     ("zkmi_g1_add", ctypes.c_int, [u64p, u64p, u64p]),
     ("zkmi_g2_add", ctypes.c_int, [u64p, u64p, u64p]),
     ("zkmi_ntt", ctypes.c_int, [vp, u64p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
@@ -90,6 +98,10 @@ SIGNATURES = [
     ("zkmi_proof_to_solana_bytes", ctypes.c_int, [u64p, u64p, u64p, u8p]),
     ("zkmi_proof_serialize_compressed", ctypes.c_int, [u64p, u64p, u64p, u8p]),
 ]
+
+
+# zkmi_allgather_fn: int (*)(void* user, const void* send, void* recv, size_t bytes)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, vp, vp, vp, sz)
 
 
 def lib(path: str | None = None):

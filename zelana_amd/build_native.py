@@ -19,6 +19,7 @@ LIB = os.environ.get("ZKMI_LIB_OUT") or os.path.join(HERE, "libzkmi.so")
 HOST = os.path.join(HERE, "host")
 HOST_LIB = os.path.join(HERE, "libzelana_prover.so")   # C++ mirror of the reference prover, above the C ABI
 HOST_TEST = os.path.join(HERE, "test_batch_prover")    # its C++ unit tests (tests/host/test_batch_prover.cpp)
+SHARD_TEST = os.path.join(HERE, "test_sharded_msm")    # 2-rank sharded MSM over zkmi.h alone (tests/host/)
 ROCM_LIB = "/opt/rocm/lib"
 ARCH = os.environ.get("ZKMI_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -64,7 +65,8 @@ def build(verbose: bool = False) -> str:
         raise RuntimeError("\n".join(errs))
     objs = [o for o, _ in results]
     if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + [
+            "-L" + ROCM_LIB, "-lrccl", "-Wl,-rpath," + ROCM_LIB]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed: " + " ".join(cmd) + "\n" + r.stdout + r.stderr)
@@ -81,8 +83,10 @@ def _build_host(verbose: bool):
     test_src = os.path.join(HERE, "..", "tests", "host", "test_batch_prover.cpp")
     inc = ["-I" + HOST, "-I" + os.path.join(HERE, "..", "include")]
     link = ["-L" + HERE, "-lzkmi", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath-link," + ROCM_LIB]
+    shard_src = os.path.join(HERE, "..", "tests", "host", "test_sharded_msm.cpp")
     for out, cmd_srcs, kind in ((HOST_LIB, srcs, ["-shared", "-fPIC"]),
-                                (HOST_TEST, [s for s in srcs if not s.endswith("capi.cpp")] + [test_src], [])):
+                                (HOST_TEST, [s for s in srcs if not s.endswith("capi.cpp")] + [test_src], []),
+                                (SHARD_TEST, [shard_src], [])):
         deps = cmd_srcs + hdrs + [LIB]
         if os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
             continue

@@ -1207,9 +1207,11 @@ using namespace zk;
 
 extern "C" {
 int zkmi_witness_map(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t* z, uint64_t* h_out) {
+  ZK_DEVICE_GUARD(ctx);
   return witness_map_host(ctx, cs, z, h_out);
 }
 int zkmi_pk_load(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, int compressed, zkmi_pk** out) {
+  ZK_DEVICE_GUARD(ctx);
   if (!ctx || !bytes || !out) {
     set_error("zkmi_pk_load: null argument");
     return ZKMI_EINVAL;
@@ -1217,6 +1219,7 @@ int zkmi_pk_load(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, int compressed
   return pk_load(ctx, bytes, len, compressed, out);
 }
 void zkmi_pk_destroy(zkmi_pk* pk) {
+  ZK_DEVICE_GUARD((pk ? pk->ctx : nullptr));
   if (!pk) return;
   zkmi_bases_destroy(pk->a_query);
   zkmi_bases_destroy(pk->b_g1_query);
@@ -1235,6 +1238,7 @@ int zkmi_pk_info(const zkmi_pk* pk, uint64_t out[3]) {
   return 0;
 }
 int zkmi_pk_precompute(zkmi_pk* pk, int factor) {
+  ZK_DEVICE_GUARD((pk ? pk->ctx : nullptr));
   if (!pk) {
     zk::set_error("zkmi_pk_precompute: null key");
     return ZKMI_EINVAL;
@@ -1267,6 +1271,7 @@ int zkmi_pk_vk_bytes(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {
   return 0;
 }
 int zkmi_r1cs_create(zkmi_ctx* ctx, const zkmi_r1cs* cs, zkmi_r1cs_dev** out) {
+  ZK_DEVICE_GUARD(ctx);
   if (!ctx || !cs || !out) {
     set_error("zkmi_r1cs_create: null argument");
     return ZKMI_EINVAL;
@@ -1286,6 +1291,7 @@ void zkmi_r1cs_destroy(zkmi_r1cs_dev* d) { delete d; }
 int zkmi_groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs_dev* cs, const void* d_z,
                                 const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
                                 uint64_t c_out[8]) {
+  ZK_DEVICE_GUARD(ctx);
   if (!ctx || !pk || !cs || !d_z || !r || !s) {
     set_error("zkmi_groth16_prove_resident: null argument");
     return ZKMI_EINVAL;
@@ -1296,10 +1302,12 @@ int zkmi_groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1c
 }
 int zkmi_pk_synthetic(zkmi_ctx* ctx, uint64_t seed, uint32_t log_n, size_t num_instance, size_t num_witness,
                       zkmi_pk** out) {
+  ZK_DEVICE_GUARD(ctx);
   return pk_synthetic(ctx, seed, log_n, num_instance, num_witness, out);
 }
 int zkmi_groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const uint64_t* z, const uint64_t r[4],
                        const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]) {
+  ZK_DEVICE_GUARD(ctx);
   if (!ctx || !pk || !cs || !z || !r || !s) {
     set_error("zkmi_groth16_prove: null argument");
     return ZKMI_EINVAL;
@@ -1310,6 +1318,7 @@ int zkmi_groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, co
 }
 int zkmi_groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t toxic[20], const uint64_t g1[8],
                        const uint64_t g2[16], zkmi_pk** out) {
+  ZK_DEVICE_GUARD(ctx);
   if (!ctx || !cs || !toxic || !g1 || !g2 || !out) {
     set_error("zkmi_groth16_setup: null argument");
     return ZKMI_EINVAL;
@@ -1317,6 +1326,7 @@ int zkmi_groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t toxic[
   return groth16_setup(ctx, cs, toxic, g1, g2, out);
 }
 int zkmi_vk_canonical(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, uint8_t* out, size_t cap, size_t* out_len) {
+  ZK_DEVICE_GUARD(ctx);
   if (!ctx || !bytes || !out_len) {
     set_error("zkmi_vk_canonical: null argument");
     return ZKMI_EINVAL;
@@ -1324,6 +1334,7 @@ int zkmi_vk_canonical(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, uint8_t* 
   return vk_canonical(ctx, bytes, len, out, cap, out_len);
 }
 int zkmi_pk_serialize(const zkmi_pk* pk, uint8_t* buf, size_t cap, size_t* len) {
+  ZK_DEVICE_GUARD((pk ? pk->ctx : nullptr));
   if (!pk || !len) {
     set_error("zkmi_pk_serialize: null argument");
     return ZKMI_EINVAL;

@@ -1806,7 +1806,9 @@ struct zkmi_msm_job {
   size_t host_words;
   hipEvent_t done;
   bool empty;
-  int sb = 1;  // segments per bit sum (added on the host)
+  int sb = 1;                   // segments per bit sum (added on the host)
+  hipStream_t st = nullptr;     // lane stream the D2H of `host` is queued on
+  zkmi_comm* comm = nullptr;    // sharded MSM: bit sums of every rank are summed
 };
 
 namespace zk {
@@ -1961,6 +1963,61 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   return 0;
 }
 
+// Bucket-reduction geometry of a plan.  Windows with rows / columns of >= 2^9
+// buckets: strip-folding waves of contiguous buckets (G1: 8 per lane, 2^20
+// table MSM 0.34 -> 0.28 ms isolated; G2: 16); otherwise <= 256-bucket strided
+// wave jobs.  sb = segments per bit sum (the longest bit job sums
+// max(2^hb * sr, 2^(lb-1) * sc) terms, cut into 256-term segments).
+struct BrGeom {
+  bool strip;
+  int sr, sc, sb;
+};
+static BrGeom br_geom(const MsmPlan& P, bool g2) {
+  static const int strip_fold = [] {  // buckets folded per lane before the tree
+    const char* e = getenv("ZKMI_BR_STRIP");
+    return e ? atoi(e) : 8;
+  }();
+  static const int strip_fold2 = [] {  // G2: 16 per lane (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
+    const char* e = getenv("ZKMI_BR_STRIP_G2");
+    return e ? atoi(e) : 16;
+  }();
+  const int fold = g2 ? strip_fold2 : strip_fold;
+  BrGeom g;
+  g.strip = fold > 0 && P.hb >= 9;
+  const int segb = g.strip ? 64 * fold : 256;  // buckets per wave job
+  g.sr = (1 << P.lb) > segb ? (1 << P.lb) / segb : 1;
+  g.sc = (1 << P.hb) > segb ? (1 << P.hb) / segb : 1;
+  const uint32_t maxterms = std::max((1u << P.hb) * g.sr, (1u << (P.lb - 1)) * g.sc);
+  g.sb = (int)((maxterms + 255) / 256);
+  return g;
+}
+
+// Queue the hand-over of a job's bit sums (W*(bb+1)*sb XYZZ terms, `words`
+// u32 at d_sums) on the lane stream: for a sharded MSM over RCCL, first the
+// all-gather of every rank's bit sums (comm stream, ordered after the lane's
+// work), then the D2H into the job's pinned buffer and the job's event.
+static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, zkmi_msm_job* job, const uint32_t* d_sums,
+                              size_t words) {
+  hipStream_t st = lane->st;
+  const int nr = job->comm ? job->comm->nranks : 1;
+  const bool dev_gather = job->comm && job->comm->kind == ZKMI_COMM_RCCL;
+  const uint32_t* src = d_sums;
+  if (dev_gather) {
+    uint32_t* gathered;
+    ZK_TRY(lane->ws.get("msm_gathered", (size_t)nr * words * 4, (void**)&gathered));
+    ZK_TRY(comm_allgather_device(job->comm, st, d_sums, gathered, words * 4));
+    src = gathered;
+  }
+  job->host_words = words;
+  const size_t host_words = dev_gather ? (size_t)nr * words : words;
+  ZK_HIP(hipEventCreateWithFlags(&job->done, hipEventDisableTiming));
+  ZK_TRY(ctx_pinned_get(ctx, host_words * 4, (void**)&job->host));
+  job->st = st;  // from here on the pinned buffer may have a copy in flight
+  ZK_HIP(hipMemcpyAsync(job->host, src, host_words * 4, hipMemcpyDeviceToHost, st));
+  ZK_HIP(hipEventRecord(job->done, st));
+  return 0;
+}
+
 // Bucket accumulation + reduction of one base set over a sorted entry list,
 // on the lane stream; queues the D2H of the bit sums and the job's event.
 template <class G>
@@ -2077,24 +2134,9 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   }
   // bucket reduction -> W*(bb+1) canonical bit sums
   uint32_t *Cb, *Db, *sums;
-  // Windows with rows / columns of >= 2^9 buckets: strip-folding waves of
-  // contiguous buckets (G1: 8 per lane, 2^20 table MSM 0.34 -> 0.28 ms
-  // isolated; G2: 16); otherwise <= 256-bucket strided wave jobs.
-  static const int strip_fold = [] {  // buckets folded per lane before the tree
-    const char* e = getenv("ZKMI_BR_STRIP");
-    return e ? atoi(e) : 8;
-  }();
-  static const int strip_fold2 = [] {  // G2: 16 per lane (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
-    const char* e = getenv("ZKMI_BR_STRIP_G2");
-    return e ? atoi(e) : 16;
-  }();
-  const int fold = G::CW == 8 ? strip_fold : strip_fold2;
-  const bool strip = fold > 0 && hb >= 9;
-  const int segb = strip ? 64 * fold : 256;  // buckets per wave job
-  const int sr = (1 << lb) > segb ? (1 << lb) / segb : 1, sc = (1 << hb) > segb ? (1 << hb) / segb : 1;
-  // bit-sum segments: the longest bit job sums max(2^hb * sr, 2^(lb-1) * sc) terms
-  const uint32_t maxterms = std::max((1u << hb) * sr, (1u << (lb - 1)) * sc);
-  const int sb = (int)((maxterms + 255) / 256);
+  const BrGeom bg = br_geom(P, G::CW != 8);
+  const bool strip = bg.strip;
+  const int sr = bg.sr, sc = bg.sc, sb = bg.sb;
   ZK_TRY(ws.get("msm_C", (size_t)W * (1u << hb) * sr * XW * 4, (void**)&Cb));
   ZK_TRY(ws.get("msm_D", (size_t)W * (1u << lb) * sc * XW * 4, (void**)&Db));
   ZK_TRY(ws.get("msm_sums", (size_t)W * (bb + 1) * sb * XW * 4, (void**)&sums));
@@ -2112,12 +2154,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     ZK_HIP(hipGetLastError());
   }
   job->sb = sb;
-  job->host_words = (size_t)W * (bb + 1) * sb * XW;
-  ZK_TRY(ctx_pinned_get(ctx, job->host_words * 4, (void**)&job->host));
-  ZK_HIP(hipMemcpyAsync(job->host, sums, job->host_words * 4, hipMemcpyDeviceToHost, st));
-  ZK_HIP(hipEventCreateWithFlags(&job->done, hipEventDisableTiming));
-  ZK_HIP(hipEventRecord(job->done, st));
-  return 0;
+  return msm_queue_handover(ctx, lane, job, sums, (size_t)W * (bb + 1) * sb * XW);
 }
 
 static int msm_acc_any(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const zkmi_bases* tb, size_t offset, size_t n,
@@ -2201,8 +2238,18 @@ int msm_submit_shared(zkmi_ctx* ctx, const zkmi_bases* const* bs, int k, size_t 
   return rc;
 }
 
+// A job freed on an error path may still have the D2H of its bit sums in
+// flight into its pinned buffer: wait for the lane before the buffer goes back
+// to the pool, or a later MSM that reuses it could have its bit sums
+// overwritten by the stale copy.
 void msm_job_free(zkmi_msm_job* job) {
   if (!job) return;
+  if (job->host && job->st) {
+    if (hipStreamSynchronize(job->st) != hipSuccess) {
+      (void)hipGetLastError();
+      job->host = nullptr;  // state unknown: drop the buffer rather than recycle it
+    }
+  }
   if (job->done) hipEventDestroy(job->done);
   if (job->host) ctx_pinned_put(job->ctx, job->host);
   delete job;
@@ -2214,6 +2261,7 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
     return ZKMI_EINVAL;
   }
   zkmi_ctx* ctx = job->ctx;
+  ZK_DEVICE_GUARD(ctx);
   int PW = job->g2 ? 32 : 16, XW = 2 * PW;
   if (job->empty) {
     memset(out, 0, PW * 4);
@@ -2223,23 +2271,44 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
   hipError_t e = hipEventSynchronize(job->done);
   if (e != hipSuccess) {
     set_error("msm_wait: %s", hipGetErrorString(e));
+    job->host = nullptr;  // copy state unknown: never recycle the buffer
     msm_job_free(job);
     return ZKMI_EHIP;
   }
+  job->st = nullptr;  // the bit-sum copy has landed
   int rc = timer_flush(ctx, false);
   auto th0 = std::chrono::steady_clock::now();
-  // terms: V_{c w + j} = U_{w,j} (j < c-1), then T_w at weight 2^{c w}
-  // (each term arrives as sb segments, summed in the combine)
-  int c = job->c, W = job->W, bb = job->bb, nbits = c * W, sb = job->sb;
-  const size_t TW = (size_t)XW * sb;  // words per term
-  std::vector<uint32_t> all((size_t)(nbits + W) * TW, 0);
-  for (int w = 0; w < W; w++) {
-    for (int j = 0; j < bb; j++)
-      memcpy(&all[((size_t)c * w + j) * TW], &job->host[((size_t)w * (bb + 1) + j) * TW], TW * 4);
-    memcpy(&all[((size_t)nbits + w) * TW], &job->host[((size_t)w * (bb + 1) + bb) * TW], TW * 4);
+  // Sharded MSM: the bit sums of all nr ranks (rank-major, host_words each).
+  // Over RCCL they were all-gathered on the device before the D2H; over a
+  // host transport the exchange happens here.
+  const int nr = job->comm ? job->comm->nranks : 1;
+  const uint32_t* src = job->host;
+  std::vector<uint32_t> gathered;
+  if (job->comm && job->comm->kind == ZKMI_COMM_HOST) {
+    gathered.resize((size_t)nr * job->host_words);
+    int grc = comm_allgather_host(job->comm, job->host, gathered.data(), job->host_words * 4);
+    if (grc) {
+      msm_job_free(job);
+      return grc;
+    }
+    src = gathered.data();
   }
-  if (!job->g2) msm_host_combine_g1(all.data(), nbits, W, c, sb, out);
-  else msm_host_combine_g2(all.data(), nbits, W, c, sb, out);
+  // terms: V_{c w + j} = U_{w,j} (j < c-1), then T_w at weight 2^{c w}
+  // (each term arrives as sb segments per rank, all summed in the combine)
+  int c = job->c, W = job->W, bb = job->bb, nbits = c * W, sb = job->sb;
+  const size_t TW = (size_t)XW * sb;  // words per term and rank
+  const size_t TA = TW * nr;          // words per term over all ranks
+  std::vector<uint32_t> all((size_t)(nbits + W) * TA, 0);
+  for (int r = 0; r < nr; r++) {
+    const uint32_t* h = src + (size_t)r * job->host_words;
+    for (int w = 0; w < W; w++) {
+      for (int j = 0; j < bb; j++)
+        memcpy(&all[((size_t)c * w + j) * TA + r * TW], &h[((size_t)w * (bb + 1) + j) * TW], TW * 4);
+      memcpy(&all[((size_t)nbits + w) * TA + r * TW], &h[((size_t)w * (bb + 1) + bb) * TW], TW * 4);
+    }
+  }
+  if (!job->g2) msm_host_combine_g1(all.data(), nbits, W, c, sb * nr, out);
+  else msm_host_combine_g2(all.data(), nbits, W, c, sb * nr, out);
   if (ctx->timer.enabled) {
     auto& t = ctx->timer.totals["msm_host_epilogue"];
     t.first += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
@@ -2254,6 +2323,85 @@ int msm_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_
   zkmi_msm_job* job;
   ZK_TRY(msm_submit(ctx, b, offset, d_scalars, n, &job));
   return msm_wait(job, out_affine);
+}
+
+// Point-sharded MSM (zkmi.h, multi-GPU): every rank agrees on one window plan
+// through a 32-byte header all-gather, runs its shard through the usual
+// pipeline, and the job hands over the bit sums of all ranks (msm_wait sums
+// them).  A rank with an empty shard contributes the same number of infinity
+// terms, so the collective still matches on every rank.
+int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+                       zkmi_msm_job** out) {
+  *out = nullptr;
+  ZK_TRY(check_range(b, offset, n));
+  zkmi_ctx* ctx = comm->ctx;
+  if (b->ctx != ctx) {
+    set_error("msm_sharded: base set belongs to another context than the communicator");
+    return ZKMI_EINVAL;
+  }
+  const MsmPlan P = msm_plan(ctx, b, n);
+  const BrGeom bg = br_geom(P, b->g2 != 0);
+  constexpr uint32_t MAGIC = 0x5A4B4D53u;
+  uint32_t hdr[8] = {MAGIC, (uint32_t)b->g2, n ? (uint32_t)P.c : 0u, n ? (uint32_t)P.W : 0u,
+                     n ? (uint32_t)P.bb : 0u, n ? (uint32_t)bg.sb : 0u, 0u, 0u};
+  if (n) ZK_TRY(check_size(P, n));
+  std::vector<uint32_t> all((size_t)8 * comm->nranks);
+  ZK_TRY(comm_allgather_host(comm, hdr, all.data(), sizeof(hdr)));
+  const uint32_t* ref = nullptr;
+  for (int r = 0; r < comm->nranks; r++) {
+    const uint32_t* h = &all[(size_t)8 * r];
+    if (h[0] != MAGIC || h[1] != hdr[1]) {
+      set_error("msm_sharded: rank %d runs a %s MSM (or is out of step)", r, h[1] ? "G2" : "G1");
+      return ZKMI_EINVAL;
+    }
+    if (!h[2]) continue;  // empty shard
+    if (!ref) ref = h;
+    else if (memcmp(ref + 2, h + 2, 4 * sizeof(uint32_t)) != 0) {
+      set_error("msm_sharded: window plans differ between ranks (c %u/%u, windows %u/%u): use equal shards "
+                "and the same fixed-base table choice on every rank", ref[2], h[2], ref[3], h[3]);
+      return ZKMI_EINVAL;
+    }
+  }
+  zkmi_msm_job* job = new_job(ctx, b, P, n);
+  job->comm = comm;
+  if (!ref) {  // every shard empty: the sum is infinity, nothing to exchange
+    job->empty = true;
+    *out = job;
+    return 0;
+  }
+  job->empty = false;
+  job->c = (int)ref[2];
+  job->W = (int)ref[3];
+  job->bb = (int)ref[4];
+  job->sb = (int)ref[5];
+  int rc = 0;
+  MsmLane* lane = nullptr;
+  if (n) {
+    uint32_t *sval, *bstart;
+    if (!(rc = get_lane(ctx, &lane)) && !(rc = msm_sort_phase(ctx, lane, P, (const uint32_t*)d_scalars, n, &sval,
+                                                               &bstart)))
+      rc = msm_acc_any(ctx, lane, P, b, offset, n, sval, bstart, job);
+  } else {
+    // infinity terms (all-zero XYZZ) of the agreed shape
+    const int XW = b->g2 ? 64 : 32;
+    const size_t words = (size_t)job->W * (job->bb + 1) * job->sb * XW;
+    uint32_t* zeros = nullptr;
+    if (!(rc = get_lane(ctx, &lane)) && !(rc = lane->ws.get("msm_zero_terms", words * 4, (void**)&zeros))) {
+      if (hipMemsetAsync(zeros, 0, words * 4, lane->st) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("msm_sharded: hipMemsetAsync failed");
+        rc = ZKMI_EHIP;
+      } else {
+        rc = msm_queue_handover(ctx, lane, job, zeros, words);
+      }
+    }
+  }
+  if (rc) {
+    msm_job_free(job);
+    return rc;
+  }
+  *out = job;
+  return 0;
 }
 
 }  // namespace zk

@@ -8,16 +8,6 @@
 
 namespace zk {
 
-// size of every pinned buffer handed out (pool bookkeeping)
-static std::map<void*, size_t>& ctx_pinned_sizes() {
-  static std::map<void*, size_t> m;
-  return m;
-}
-static size_t ctx_pinned_sizes_lookup(void* p, size_t dflt) {
-  auto it = ctx_pinned_sizes().find(p);
-  return it == ctx_pinned_sizes().end() ? dflt : it->second;
-}
-
 static thread_local char g_err[512] = "";
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -94,12 +84,13 @@ int ctx_sync_all(zkmi_ctx* ctx) {
   return 0;
 }
 
+// Pinned staging buffers, pooled per context (a context is single-threaded,
+// so its pool needs no lock; two contexts never share one).
 int ctx_pinned_get(zkmi_ctx* ctx, size_t bytes, void** out) {
   for (size_t i = 0; i < ctx->pinned_free.size(); i++) {
     if (ctx->pinned_free[i].second >= bytes) {
       *out = ctx->pinned_free[i].first;
       ctx->pinned_free.erase(ctx->pinned_free.begin() + i);
-      ctx_pinned_sizes()[*out] = ctx_pinned_sizes_lookup(*out, bytes);
       return 0;
     }
   }
@@ -109,14 +100,12 @@ int ctx_pinned_get(zkmi_ctx* ctx, size_t bytes, void** out) {
     set_error("hipHostMalloc(%zu) failed", sz);
     return ZKMI_ENOMEM;
   }
-  ctx_pinned_sizes()[*out] = sz;
+  ctx->pinned_size[*out] = sz;
   return 0;
 }
 void ctx_pinned_put(zkmi_ctx* ctx, void* p) {
-  auto& m = ctx_pinned_sizes();
-  auto it = m.find(p);
-  size_t sz = it == m.end() ? 0 : it->second;
-  ctx->pinned_free.push_back({p, sz});
+  auto it = ctx->pinned_size.find(p);
+  ctx->pinned_free.push_back({p, it == ctx->pinned_size.end() ? 0 : it->second});
 }
 
 }  // namespace zk
@@ -149,7 +138,7 @@ int zkmi_ctx_create(int device, zkmi_ctx** out) {
     set_error("device %d is %s; libzkmi is built for gfx950 (MI355X) only", device, prop.gcnArchName);
     return ZKMI_ENODEV;
   }
-  ZK_HIP(hipSetDevice(device));
+  DeviceGuard guard(device);  // the stream belongs to `device`; the caller's device is restored
   zkmi_ctx* c = new zkmi_ctx;
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
@@ -163,7 +152,7 @@ int zkmi_ctx_create(int device, zkmi_ctx** out) {
 }
 void zkmi_ctx_destroy(zkmi_ctx* ctx) {
   if (!ctx) return;
-  hipSetDevice(ctx->device);
+  ZK_DEVICE_GUARD(ctx);
   ctx_sync_all(ctx);
   timer_flush(ctx);
   ctx->ws.release_all();
@@ -177,6 +166,7 @@ void zkmi_ctx_destroy(zkmi_ctx* ctx) {
   ctx->lanes.clear();
   for (auto& pb : ctx->pinned_free) hipHostFree(pb.first);
   ctx->pinned_free.clear();
+  ctx->pinned_size.clear();
   hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -185,6 +175,7 @@ int zkmi_profile_enable(zkmi_ctx* ctx, int on) {
   return 0;
 }
 int zkmi_profile_get(zkmi_ctx* ctx, const char* name, double* total_ms, uint64_t* count) {
+  ZK_DEVICE_GUARD(ctx);
   ZK_TRY(timer_flush(ctx));
   auto it = ctx->timer.totals.find(name);
   *total_ms = it == ctx->timer.totals.end() ? 0.0 : it->second.first;
@@ -192,12 +183,13 @@ int zkmi_profile_get(zkmi_ctx* ctx, const char* name, double* total_ms, uint64_t
   return 0;
 }
 int zkmi_profile_reset(zkmi_ctx* ctx) {
+  ZK_DEVICE_GUARD(ctx);
   ZK_TRY(timer_flush(ctx));
   ctx->timer.totals.clear();
   return 0;
 }
 int zkmi_dev_alloc(zkmi_ctx* ctx, size_t bytes, void** dptr) {
-  hipSetDevice(ctx->device);
+  ZK_DEVICE_GUARD(ctx);
   if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess) {
     (void)hipGetLastError();
     set_error("hipMalloc(%zu) failed", bytes);
@@ -206,36 +198,45 @@ int zkmi_dev_alloc(zkmi_ctx* ctx, size_t bytes, void** dptr) {
   return 0;
 }
 int zkmi_dev_free(zkmi_ctx* ctx, void* dptr) {
-  (void)ctx;
+  ZK_DEVICE_GUARD(ctx);
   ZK_HIP(hipFree(dptr));
   return 0;
 }
 int zkmi_h2d(zkmi_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  ZK_DEVICE_GUARD(ctx);
   ZK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
   ZK_HIP(hipStreamSynchronize(ctx->stream));
   return 0;
 }
 int zkmi_d2h(zkmi_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  ZK_DEVICE_GUARD(ctx);
   ZK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   ZK_HIP(hipStreamSynchronize(ctx->stream));
   return 0;
 }
-int zkmi_sync(zkmi_ctx* ctx) { return ctx_sync_all(ctx); }
+int zkmi_sync(zkmi_ctx* ctx) {
+  ZK_DEVICE_GUARD(ctx);
+  return ctx_sync_all(ctx);
+}
 
 // ------------------------------------------------------------------ MSM
 int zkmi_bases_create_g1(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_bases** out) {
+  ZK_DEVICE_GUARD(ctx);
   return bases_upload(ctx, 0, affine, n, out);
 }
 int zkmi_bases_create_g2(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_bases** out) {
+  ZK_DEVICE_GUARD(ctx);
   return bases_upload(ctx, 1, affine, n, out);
 }
 void zkmi_bases_destroy(zkmi_bases* b) {
+  ZK_DEVICE_GUARD(b);
   if (!b) return;
   hipFree(b->d_pts);
   delete b;
 }
 size_t zkmi_bases_len(const zkmi_bases* b) { return b ? b->n : 0; }
 int zkmi_bases_export(const zkmi_bases* b, uint64_t* affine_out) {
+  ZK_DEVICE_GUARD(b);
   if (!b) {
     set_error("zkmi_bases_export: null bases");
     return ZKMI_EINVAL;
@@ -243,6 +244,7 @@ int zkmi_bases_export(const zkmi_bases* b, uint64_t* affine_out) {
   return bases_export(b, affine_out);
 }
 int zkmi_bases_precompute(zkmi_bases* b, int c, int factor) {
+  ZK_DEVICE_GUARD(b);
   if (!b) {
     set_error("zkmi_bases_precompute: null bases");
     return ZKMI_EINVAL;
@@ -265,18 +267,23 @@ int zkmi_bases_info(const zkmi_bases* b, uint64_t out[4]) {
   return 0;
 }
 int zkmi_bases_generate_g1(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** out) {
+  ZK_DEVICE_GUARD(ctx);
   return bases_generate(ctx, 0, seed, n, out);
 }
 int zkmi_bases_generate_g2(zkmi_ctx* ctx, uint64_t seed, size_t n, zkmi_bases** out) {
+  ZK_DEVICE_GUARD(ctx);
   return bases_generate(ctx, 1, seed, n, out);
 }
 int zkmi_scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_scalars) {
+  ZK_DEVICE_GUARD(ctx);
   return scalars_generate(ctx, seed, 0, n, d_scalars);
 }
 int zkmi_bases_generate_range_g1(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, zkmi_bases** out) {
+  ZK_DEVICE_GUARD(ctx);
   return bases_generate(ctx, 0, seed, first, n, out);
 }
 int zkmi_scalars_generate_range(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, void* d_scalars) {
+  ZK_DEVICE_GUARD(ctx);
   return scalars_generate(ctx, seed, first, n, d_scalars);
 }
 
@@ -289,6 +296,7 @@ static int msm_host_scalars(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, c
 }
 int zkmi_msm_g1(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_t* scalars, size_t n,
                 uint64_t out_affine[8]) {
+  ZK_DEVICE_GUARD(ctx);
   if (!b || b->g2) {
     set_error("zkmi_msm_g1: G1 base set required");
     return ZKMI_EINVAL;
@@ -297,6 +305,7 @@ int zkmi_msm_g1(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_
 }
 int zkmi_msm_g2(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_t* scalars, size_t n,
                 uint64_t out_affine[16]) {
+  ZK_DEVICE_GUARD(ctx);
   if (!b || !b->g2) {
     set_error("zkmi_msm_g2: G2 base set required");
     return ZKMI_EINVAL;
@@ -305,6 +314,7 @@ int zkmi_msm_g2(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const uint64_
 }
 int zkmi_msm_g1_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                        uint64_t out_affine[8]) {
+  ZK_DEVICE_GUARD(ctx);
   if (!b || b->g2) {
     set_error("zkmi_msm_g1_device: G1 base set required");
     return ZKMI_EINVAL;
@@ -313,6 +323,7 @@ int zkmi_msm_g1_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const 
 }
 int zkmi_msm_g2_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                        uint64_t out_affine[16]) {
+  ZK_DEVICE_GUARD(ctx);
   if (!b || !b->g2) {
     set_error("zkmi_msm_g2_device: G2 base set required");
     return ZKMI_EINVAL;
@@ -321,11 +332,13 @@ int zkmi_msm_g2_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const 
 }
 int zkmi_msm_submit(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                     zkmi_msm_job** job) {
+  ZK_DEVICE_GUARD(ctx);
   return msm_submit(ctx, b, offset, d_scalars, n, job);
 }
 int zkmi_msm_wait(zkmi_msm_job* job, uint64_t* out_affine) { return msm_wait(job, out_affine); }
 int zkmi_msm_submit_shared(zkmi_ctx* ctx, const zkmi_bases* const* bs, int k, size_t offset, const void* d_scalars,
                            size_t n, zkmi_msm_job** jobs) {
+  ZK_DEVICE_GUARD(ctx);
   if (!ctx || !bs || !jobs || k < 1 || (n && !d_scalars)) {
     set_error("zkmi_msm_submit_shared: bad arguments");
     return ZKMI_EINVAL;
@@ -359,11 +372,13 @@ int zkmi_g2_add(const uint64_t a[16], const uint64_t b[16], uint64_t out[16]) {
 
 // ------------------------------------------------------------------ NTT
 int zkmi_ntt_device(zkmi_ctx* ctx, void* d_data, uint32_t log_n, int inverse, int coset) {
+  ZK_DEVICE_GUARD(ctx);
   ZK_TRY(ntt_device(ctx, (uint32_t*)d_data, log_n, inverse, coset));
   ZK_HIP(hipStreamSynchronize(ctx->stream));
   return timer_flush(ctx);
 }
 int zkmi_ntt(zkmi_ctx* ctx, uint64_t* data, uint32_t log_n, int inverse, int coset) {
+  ZK_DEVICE_GUARD(ctx);
   if (log_n > 28) {
     set_error("ntt: log_n %u > 28", log_n);
     return ZKMI_EINVAL;

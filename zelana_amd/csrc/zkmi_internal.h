@@ -62,7 +62,8 @@ struct zkmi_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   zk::Workspace ws;
-  std::vector<std::pair<void*, size_t>> pinned_free;  // pool of pinned host buffers
+  std::vector<std::pair<void*, size_t>> pinned_free;  // pool of pinned host buffers (ptr, size)
+  std::map<void*, size_t> pinned_size;                 // size of every pinned buffer handed out
   zk::KernelTimer timer;
   int msm_window = 0;  // 0 = auto
   int num_cus = 256;
@@ -84,7 +85,59 @@ struct zkmi_bases {
   int tw = 0;  // windows per copy
 };
 
+// Multi-rank communicator (zkmi.h multi-GPU section; comm.hip).
+constexpr int ZKMI_COMM_RCCL = 0;
+constexpr int ZKMI_COMM_HOST = 1;
+struct zkmi_comm {
+  zkmi_ctx* ctx = nullptr;
+  int nranks = 1, rank = 0, kind = ZKMI_COMM_RCCL;
+  void* nccl = nullptr;                 // ncclComm_t (RCCL transport): bit-sum exchanges
+  void* nccl_ctl = nullptr;             // split of it for the synchronous plan headers
+  hipStream_t st = nullptr;             // every bit-sum exchange, in issue order
+  hipStream_t st_ctl = nullptr;         // header exchanges (never wait behind queued MSMs)
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  uint32_t* d_stage = nullptr;          // device staging for host-buffer collectives
+  size_t stage_bytes = 0;
+  zkmi_allgather_fn fn = nullptr;       // host transport
+  void* user = nullptr;
+};
+
 namespace zk {
+// All-gather of `bytes` per rank from device memory, ordered after the work
+// already queued on `lane_st` and before anything queued there afterwards
+// (RCCL transport only).
+int comm_allgather_device(zkmi_comm* c, hipStream_t lane_st, const void* d_send, void* d_recv, size_t bytes);
+// Synchronous all-gather of host buffers (either transport).
+int comm_allgather_host(zkmi_comm* c, const void* send, void* recv, size_t bytes);
+int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
+                       zkmi_msm_job** out);
+
+// HIP's current device is per host thread (default 0).  Every entry point that
+// works on a context, key or base set selects that context's device for the
+// duration of the call and restores the caller's device on return, so a
+// context made for device k can be driven from any thread (e.g. a tokio
+// blocking-pool thread) without touching GPU 0.
+struct DeviceGuard {
+  int prev = -1;
+  bool restore = false;
+  explicit DeviceGuard(int dev) {
+    if (dev < 0) return;
+    if (hipGetDevice(&prev) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    if (prev != dev && hipSetDevice(dev) == hipSuccess) restore = true;
+  }
+  ~DeviceGuard() {
+    if (restore) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+inline int dev_of(const zkmi_ctx* c) { return c ? c->device : -1; }
+inline int dev_of(const zkmi_bases* b) { return b && b->ctx ? b->ctx->device : -1; }
+#define ZK_DEVICE_GUARD(obj) ::zk::DeviceGuard zk_device_guard_(::zk::dev_of(obj))
+
 // kernel timing helpers (events on ctx->stream)
 void timer_begin(zkmi_ctx* ctx, const char* name, hipEvent_t* ev, hipStream_t st);
 void timer_end(zkmi_ctx* ctx, const char* name, hipEvent_t ev, hipStream_t st);

@@ -1,17 +1,52 @@
-"""Multi-GPU MSM: point sharding + one exchange step.
+"""Multi-GPU glue between torch.distributed (process launch / rendezvous,
+as bench.py uses it) and libzkmi's own communicator (zkmi.h multi-GPU
+section), which does the MSM exchange natively.
 
 Each rank (one process per GPU) owns a shard of the bases, resident in its
-HBM, and runs a full Pippenger MSM on it.  The only exchange is the partial
-result: RCCL has no elliptic-curve reduction, so the "all-reduce of partial
-bucket sums" is an all-gather of one 64-byte affine point per rank (RCCL over
-xGMI when the backend is nccl) followed by an exact group-law sum on the host
-(zkmi_g1_add).  The payload is tiny, so the collective is latency-bound.
+HBM, and runs a full Pippenger MSM on it.  The exchange is one
+all-gather of every rank's per-window bit sums inside libzkmi: ncclAllGather
+over xGMI on the MSM lane's stream (backend "nccl" = RCCL), or a host
+all-gather supplied by the caller (here torch.distributed over gloo, for ranks
+sharing one GPU).  RCCL has no elliptic-curve reduction, so the sum of the
+gathered bit sums is the group law in libzkmi's epilogue.
+
+`combine_partials` (all-gather of finished per-rank affine results + host
+group-law sum) remains for callers that already hold per-rank results.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from .gpu import g1_add, g2_add
+from .gpu import Comm, comm_unique_id, g1_add, g2_add
+
+
+def torch_allgather(group=None):
+    """bytes -> list[bytes] of every rank (torch.distributed all-gather of a
+    fixed-size uint8 tensor; the zkmi host transport's callback)."""
+    import torch
+    import torch.distributed as dist
+
+    def ag(blob: bytes):
+        world = dist.get_world_size(group)
+        t = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+        bufs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(bufs, t, group=group)
+        return [bytes(b.numpy().tobytes()) for b in bufs]
+    return ag
+
+
+def make_comm(ctx, backend: str) -> Comm:
+    """libzkmi communicator over the current torch.distributed world:
+    RCCL when the backend is nccl (the unique id is broadcast by rank 0),
+    otherwise the host transport over torch.distributed."""
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if backend == "nccl":
+        obj = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return Comm.rccl(ctx, obj[0], world, rank)
+    return Comm.host(ctx, world, rank, torch_allgather())
 
 
 def allgather_points(point: np.ndarray, device=None) -> list[np.ndarray]:

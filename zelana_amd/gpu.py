@@ -192,6 +192,88 @@ class Context:
         check(lib().zkmi_ntt_device(self.h, buf.ptr, log_n, int(inverse), int(coset)), "zkmi_ntt_device")
 
 
+def shard_range(total: int, nranks: int, rank: int):
+    """(first, count) of rank's contiguous point shard (zkmi_shard_range)."""
+    f, c = ctypes.c_size_t(), ctypes.c_size_t()
+    check(lib().zkmi_shard_range(total, nranks, rank, ctypes.byref(f), ctypes.byref(c)), "zkmi_shard_range")
+    return f.value, c.value
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (one rank creates it, the host broadcasts it)."""
+    buf = (ctypes.c_uint8 * 128)()
+    check(lib().zkmi_comm_unique_id(buf), "zkmi_comm_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """Multi-rank communicator of a context (zkmi.h multi-GPU section).
+
+    Comm.rccl(ctx, uid, nranks, rank): RCCL transport (one rank per GPU).
+    Comm.host(ctx, nranks, rank, allgather): host transport; `allgather(bytes)
+    -> list[bytes]` of every rank (e.g. torch.distributed over gloo), for
+    ranks that share a GPU or hosts without RCCL."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.h = vp()
+        self._cb = None
+
+    @classmethod
+    def rccl(cls, ctx: Context, uid: bytes, nranks: int, rank: int) -> "Comm":
+        c = cls(ctx)
+        ub = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().zkmi_comm_init(ctx.h, ub, nranks, rank, ctypes.byref(c.h)), "zkmi_comm_init")
+        return c
+
+    @classmethod
+    def host(cls, ctx: Context, nranks: int, rank: int, allgather) -> "Comm":
+        from ._lib import ALLGATHER_FN
+
+        c = cls(ctx)
+
+        def cb(_user, send, recv, nbytes):
+            try:
+                parts = allgather(ctypes.string_at(send, nbytes))
+                blob = b"".join(parts)
+                assert len(blob) == nbytes * nranks
+                ctypes.memmove(recv, blob, len(blob))
+                return 0
+            except Exception:  # reported to the caller as the entry point's error
+                return 1
+
+        c._cb = ALLGATHER_FN(cb)
+        check(lib().zkmi_comm_init_host(ctx.h, nranks, rank, ctypes.cast(c._cb, vp), None, ctypes.byref(c.h)),
+              "zkmi_comm_init_host")
+        return c
+
+    def info(self):
+        """(nranks, rank, transport: 0 RCCL, 1 host)"""
+        out = (ctypes.c_int * 3)()
+        check(lib().zkmi_comm_info(self.h, out), "zkmi_comm_info")
+        return tuple(out)
+
+    def msm_submit(self, shard: "Bases", dscalars: "DeviceBuffer", n: int, offset: int = 0):
+        job = vp()
+        check(lib().zkmi_msm_sharded_submit(self.h, shard.h, offset, dscalars.ptr if n else None, n,
+                                            ctypes.byref(job)), "zkmi_msm_sharded_submit")
+        return (job, shard.g2)
+
+    def msm(self, shard: "Bases", dscalars: "DeviceBuffer", n: int, offset: int = 0):
+        return self.ctx.msm_wait(self.msm_submit(shard, dscalars, n, offset))
+
+    def close(self):
+        if self.h:
+            lib().zkmi_comm_destroy(self.h)
+            self.h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def g1_add(a, b):
     out = np.zeros(8, np.uint64)
     check(lib().zkmi_g1_add(_p64(np.ascontiguousarray(a, np.uint64)), _p64(np.ascontiguousarray(b, np.uint64)),

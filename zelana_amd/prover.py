@@ -208,44 +208,3 @@ def _as_z(z):
     if isinstance(z, np.ndarray):
         return z
     return np.array([[(v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)] for v in z], np.uint64)
-
-
-def smoke_square_circuit(ctx: gpu.Context):
-    """Used by __graft_entry__.smoke(): SquareCircuit proof with pk from the
-    oracle setup must reproduce the reference's proof_for_onchain.json."""
-    import ctypes
-    import os
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, os.path.join(root, "tests"))
-    import oracle_ctypes as O
-
-    from .r1cs import square_circuit
-
-    cs, z = square_circuit(7)
-    st, keep = O.make_r1cs(cs)
-    rng = O.Rng(42)
-    opk = O.lib().oracle_groth16_setup(ctypes.byref(st), rng.h, 1)
-    buf = np.zeros(1 << 16, np.uint8)
-    nb = O.lib().oracle_pk_serialize(opk, 1, buf.ctypes.data, buf.size)
-    pk = gpu.ProvingKey(ctx, buf[:nb].tobytes(), True)
-    # the proof continues the setup's rng (snarkjs.rs:153-159): r then s
-    rs = np.zeros(8, np.uint64)
-    O.lib().oracle_fr_rand(rng.h, O.P(rs[:4]))
-    O.lib().oracle_fr_rand(rng.h, O.P(rs[4:]))
-    a, b, c = gpu.groth16_prove(ctx, pk, cs, _as_z(z), O.limbs_to_int(rs[:4]), O.limbs_to_int(rs[4:]))
-    with open(os.path.join(root, "tests", "golden", "ref_proof_for_onchain.json")) as f:
-        ref = json.load(f)["proof_components"]
-    ba = np.zeros(64, np.uint8)
-    O.lib().oracle_g1_serialize(O.P(a), 0, O.P(ba))
-    assert list(ba) == ref["pi_a"], "GPU proof pi_a != reference fixture"
-    bb = np.zeros(128, np.uint8)
-    O.lib().oracle_g2_serialize(O.P(b), 0, O.P(bb))
-    assert list(bb) == ref["pi_b"], "GPU proof pi_b != reference fixture"
-    bc = np.zeros(64, np.uint8)
-    O.lib().oracle_g1_serialize(O.P(c), 0, O.P(bc))
-    assert list(bc) == ref["pi_c"], "GPU proof pi_c != reference fixture"
-    O.lib().oracle_pk_free(opk)
-    pk.close()
-    del keep
