@@ -72,6 +72,14 @@ def parse():
     return ap.parse_args()
 
 
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """progress on stderr (stdout carries only the JSON line)"""
+    print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -153,6 +161,7 @@ def main():
                 out[name] = round(t / k, 4)
         return out
 
+    log(f"rank {rank}/{world}: inputs resident; headline MSM 2^{args.log_n}")
     # plain Pippenger first (no table: every window recomputed, as arkworks does)
     plain = None
     if not args.no_plain:
@@ -207,17 +216,22 @@ def main():
     # best there: their MSMs are long enough that two overlap fully)
     ctx.set_lanes(2)
     if not args.no_big:
+        log("config 5: global 2^%d MSM" % args.big_log_n)
         extra["msm_global_2_%d" % args.big_log_n] = bench_msm_sharded(
             ctx, args.big_log_n, args.big_steps, world, rank, submit, finish, sync_all, allmax, 2)
     ntt_state = zb_state = None
     if not args.no_ntt:
+        log("NTT + INTT")
         extra["ntt"], ntt_state = bench_ntt(ctx, args.ntt_log_n, world, sync_all, allmax)
     if not args.no_l2:
+        log("L2-scale proofs")
         extra["l2_proofs"] = bench_l2(ctx, args.l2_log_n, args.l2_steps, rank, world, sync_all, allmax)
     if not args.no_zbatch:
+        log("zelana_batch proofs")
         extra["zelana_batch_proofs"], zb_state = bench_zbatch(ctx, args.l2_steps, world, sync_all, allmax)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("CPU baseline legs")
         cpu = cpu_baseline(ctx, bases, scalars, n, result, args.cpu_threads, ntt_state,
                            None if args.no_cpu_prove else zb_state)
 
@@ -620,6 +634,7 @@ def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb
         "legs": {},
     }
     if ntt_state is not None:
+        log("CPU NTT leg")
         log_n, x, fwd = ntt_state["log_n"], ntt_state["x"], ntt_state["fwd"]
         t0 = time.perf_counter()
         cf = O.ntt(x, log_n, False, False, threads=threads)
@@ -633,6 +648,7 @@ def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb
             "gpu_matches_cpu": bool(np.array_equal(cf.reshape(-1, 4), fwd) and np.array_equal(ci.reshape(-1, 4), x)),
         }
     if zb_state is not None:
+        log("CPU prove leg: oracle setup + prove")
         cs, z, r, s = zb_state["cs"], zb_state["z"], zb_state["r"], zb_state["s"]
         st, keep = O.make_r1cs(cs)
         rng = O.Rng(0)
