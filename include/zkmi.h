@@ -276,6 +276,36 @@ int zkmi_proof_to_solana_bytes(const uint64_t a[8], const uint64_t b[16], const 
 int zkmi_proof_serialize_compressed(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8],
                                     uint8_t out[128]);
 
+/* ------------------------------------------------- verification / on-chain
+ * Host code (no GPU needed).  The reference's Groth16Prover::verify is a
+ * length check (prover.rs:427-442); the real check is the on-chain verifier's
+ * (onchain-programs/verifier/programs/onchain_verifier/src/lib.rs:497-547),
+ * restated here so a host can check its proofs before settling them. */
+/* ark-groth16 verify_proof: vk = arkworks-compressed VerifyingKey bytes (as
+ * Groth16Prover::from_bytes reads them; decoded and validated, G2 subgroup
+ * included); inputs = n canonical Fr (4 x u64), n = IC count - 1.
+ * *valid = 1 iff e(A,B) = e(alpha,beta) e(IC[0] + sum x_i IC[i+1], gamma) e(C,delta). */
+int zkmi_groth16_verify(const uint8_t* vk, size_t vk_len, const uint64_t* inputs, size_t n_inputs,
+                        const uint64_t a[8], const uint64_t b[16], const uint64_t c[8], int* valid);
+/* The alt_bn128 syscalls the on-chain verifier calls (EIP-196/197 big-endian:
+ * G1 = x || y, G2 = x.c1 || x.c0 || y.c1 || y.c0, (0,0) = infinity; points
+ * validated, G2 in the order-r subgroup).  pairing: k x 192 bytes -> 32-byte
+ * big-endian 1 iff prod e(P_i, Q_i) = 1. */
+int zkmi_alt_bn128_pairing(const uint8_t* input, size_t len, uint8_t out[32]);
+int zkmi_alt_bn128_g1_add(const uint8_t in[128], uint8_t out[64]);
+int zkmi_alt_bn128_g1_mul(const uint8_t in[96], uint8_t out[64]);
+/* The 256-B proof in the syscalls' big-endian encoding: -A || B || C
+ * (the big-endian flag of proof_to_solana_bytes, whose reference output is
+ * little-endian: SURVEY.md App. B.3). */
+int zkmi_proof_to_alt_bn128_bytes(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8], uint8_t out[256]);
+/* batch_inputs_to_field_elements (verifier lib.rs:479-494): the six 32-byte
+ * roots as given, then batch_id as a 32-byte big-endian field element */
+int zkmi_batch_inputs_alt_bn128(const uint8_t roots[6 * 32], uint64_t batch_id, uint8_t out[7 * 32]);
+/* k * P on G1 (canonical affine): ProverNode::generate_fragment's single scalar
+ * multiplication (forge/prover/src/lib.rs:351-358); with zkmi_g1_add it covers
+ * the forge's <= 7-point Lagrange sums (:252-290) */
+int zkmi_g1_mul(const uint64_t p[8], const uint64_t k[4], uint64_t out[8]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <map>
+
 #include <fstream>
 #include <iterator>
 
@@ -119,6 +121,40 @@ static void test_gpu(const char* pk_path, const char* vk_path) {
   CHECK(prover->verify(p));
   BatchProof q = prover->prove(in, w);  // deterministic: StdRng(batch_id)
   CHECK(p.proof_bytes == q.proof_bytes);
+  // pairing check (verify_pairing, the on-chain relation): a batch whose
+  // public roots are the ones the circuit derives verifies; the zero-root
+  // batch above is unsatisfied (prover.rs passes blake3 batch hashes, App. B.2)
+  // and must not
+  std::map<std::string, Fr> comp;
+  Groth16Prover::circuit_of(in, w).synthesize(&comp);
+  auto le = [](const Fr& f) {
+    uint64_t c[4];
+    f.to_canon(c);
+    Bytes32 b;
+    for (int i = 0; i < 32; i++) b[i] = (uint8_t)(c[i / 8] >> (8 * (i % 8)));
+    return b;
+  };
+  BatchPublicInputs good = in;
+  good.pre_state_root = le(comp["pre_state_root"]);
+  good.post_state_root = le(comp["post_state_root"]);
+  good.post_shielded_root = le(comp["post_shielded_root"]);
+  good.withdrawal_root = le(comp["withdrawal_root"]);
+  good.batch_hash = le(comp["batch_hash"]);
+  const R1CSMatrices gm = Groth16Prover::circuit_of(good, w).synthesize();
+  CHECK(gm.is_satisfied());
+  auto instances = [](const R1CSMatrices& m) {
+    std::vector<std::array<uint64_t, 4>> v(m.num_instance - 1);
+    for (size_t i = 1; i < m.num_instance; i++) memcpy(v[i - 1].data(), &m.z[4 * i], 32);
+    return v;
+  };
+  BatchProof gp = prover->prove(good, w);
+  CHECK(prover->verify_pairing(gp, instances(gm)));
+  const R1CSMatrices bm = Groth16Prover::circuit_of(in, w).synthesize();
+  CHECK(!bm.is_satisfied());
+  CHECK(!prover->verify_pairing(p, instances(bm)));
+  auto tampered = instances(gm);
+  tampered[6][0] ^= 1;  // batch_id
+  CHECK(!prover->verify_pairing(gp, tampered));
   bool threw = false;
   try {
     Groth16Prover::from_bytes({1, 2, 3}, vk);

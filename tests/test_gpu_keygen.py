@@ -157,6 +157,12 @@ def test_zbatch_full_keygen_prove_verify(ctx):
     O.lib().oracle_pk_free(opk)
     assert np.array_equal(a, oa) and np.array_equal(b, ob) and np.array_equal(c, oc), "GPU proof != oracle proof"
     assert gpu.proof_to_solana_bytes(a, b, c) == gpu.proof_to_solana_bytes(oa, ob, oc)
+    # the product's own verifier (host pairing, zkmi_groth16_verify) accepts it
+    pub_native = [O.limbs_to_int(z[i]) for i in range(1, cs.num_instance)]
+    assert gpu.groth16_verify(vk, pub_native, a, b, c)
+    pub_native[2] = (pub_native[2] + 1) % O.R
+    assert not gpu.groth16_verify(vk, pub_native, a, b, c)
+    step("native verify done")
     pub = [O.limbs_to_int(z[i]) for i in range(1, cs.num_instance)]
     vkd = _vk_points(vk, cs.num_instance)
     g1_add, g1_mul = PR.oracle_g1_ops()

@@ -95,6 +95,13 @@ SIGNATURES = [
     ("zkmi_groth16_setup", ctypes.c_int, [vp, vp, u64p, u64p, u64p, ctypes.POINTER(vp)]),
     ("zkmi_pk_serialize", ctypes.c_int, [vp, u8p, sz, ctypes.POINTER(sz)]),
     ("zkmi_vk_canonical", ctypes.c_int, [vp, u8p, sz, u8p, sz, ctypes.POINTER(sz)]),
+    ("zkmi_groth16_verify", ctypes.c_int, [u8p, sz, u64p, sz, u64p, u64p, u64p, ctypes.POINTER(ctypes.c_int)]),
+    ("zkmi_alt_bn128_pairing", ctypes.c_int, [u8p, sz, u8p]),
+    ("zkmi_alt_bn128_g1_add", ctypes.c_int, [u8p, u8p]),
+    ("zkmi_alt_bn128_g1_mul", ctypes.c_int, [u8p, u8p]),
+    ("zkmi_proof_to_alt_bn128_bytes", ctypes.c_int, [u64p, u64p, u64p, u8p]),
+    ("zkmi_batch_inputs_alt_bn128", ctypes.c_int, [u8p, ctypes.c_uint64, u8p]),
+    ("zkmi_g1_mul", ctypes.c_int, [u64p, u64p, u64p]),
     ("zkmi_proof_to_solana_bytes", ctypes.c_int, [u64p, u64p, u64p, u8p]),
     ("zkmi_proof_serialize_compressed", ctypes.c_int, [u64p, u64p, u64p, u8p]),
 ]

@@ -414,6 +414,27 @@ def witness_map(ctx: Context, cs, z: np.ndarray) -> np.ndarray:
     return h
 
 
+def groth16_verify(vk_bytes: bytes, public_inputs, a, b, c) -> bool:
+    """zkmi_groth16_verify (host pairing check of the on-chain verifier's
+    relation; vk_bytes = arkworks-compressed VerifyingKey, inputs = ints)."""
+    vk = np.frombuffer(bytes(vk_bytes), np.uint8).copy()
+    ins = np.array([_limbs(int(x)) for x in public_inputs], np.uint64).reshape(-1, 4)
+    ok = ctypes.c_int(0)
+    check(lib().zkmi_groth16_verify(vk.ctypes.data_as(u8p), vk.size, _p64(ins), len(public_inputs),
+                                    _p64(np.ascontiguousarray(a, np.uint64)), _p64(np.ascontiguousarray(b, np.uint64)),
+                                    _p64(np.ascontiguousarray(c, np.uint64)), ctypes.byref(ok)), "zkmi_groth16_verify")
+    return bool(ok.value)
+
+
+def proof_to_alt_bn128_bytes(a, b, c) -> bytes:
+    """-A || B || C in the alt_bn128 syscalls' big-endian encoding."""
+    out = np.zeros(256, np.uint8)
+    check(lib().zkmi_proof_to_alt_bn128_bytes(_p64(np.ascontiguousarray(a, np.uint64)),
+                                              _p64(np.ascontiguousarray(b, np.uint64)),
+                                              _p64(np.ascontiguousarray(c, np.uint64)), out.ctypes.data_as(u8p)))
+    return out.tobytes()
+
+
 def proof_to_solana_bytes(a, b, c) -> bytes:
     out = np.zeros(256, np.uint8)
     check(lib().zkmi_proof_to_solana_bytes(_p64(np.ascontiguousarray(a, np.uint64)),

@@ -1,6 +1,8 @@
 // batch_prover.cpp — see batch_prover.h.
 #include "batch_prover.h"
 
+#include <string.h>
+
 #include <chrono>
 #include <fstream>
 #include <iterator>
@@ -122,13 +124,47 @@ BatchProof Groth16Prover::prove(const BatchPublicInputs& inputs, const BatchWitn
     *vals[t] = m.val[t].data();
   }
   uint64_t a[8], b[16], c[8];
-  if (zkmi_groth16_prove(ctx_, pk_, &cs, m.z.data(), r, s, a, b, c) != 0) fail("Proving failed");
+  {
+    std::lock_guard<std::mutex> lock(gpu_mu_);  // synthesis above runs unlocked, in parallel
+    if (zkmi_groth16_prove(ctx_, pk_, &cs, m.z.data(), r, s, a, b, c) != 0) fail("Proving failed");
+  }
   BatchProof p;
   p.public_inputs = inputs;
   p.proof_bytes = proof_to_solana_bytes(a, b, c);
   p.proving_time_ms =
       (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - start).count();
   return p;
+}
+
+bool Groth16Prover::verify_pairing(const BatchProof& proof,
+                                   const std::vector<std::array<uint64_t, 4>>& inputs) const {
+  if (proof.proof_bytes.size() != 256) return false;
+  // undo proof_to_solana_bytes: -A || B || C, little-endian coordinates
+  uint64_t w[32];
+  for (int i = 0; i < 32; i++) {
+    w[i] = 0;
+    for (int j = 0; j < 8; j++) w[i] |= (uint64_t)proof.proof_bytes[8 * i + j] << (8 * j);
+  }
+  uint64_t a[8], b[16], c[8];
+  memcpy(a, w, 64);
+  memcpy(b, w + 8, 128);
+  memcpy(c, w + 24, 64);
+  static const uint64_t Q[4] = {0x3c208c16d87cfd47ULL, 0x97816a916871ca8dULL, 0xb85045b68181585dULL,
+                                0x30644e72e131a029ULL};
+  if (a[4] | a[5] | a[6] | a[7]) {  // y -> q - y (A = -(-A))
+    unsigned __int128 br = 0;
+    for (int i = 0; i < 4; i++) {
+      unsigned __int128 d = (unsigned __int128)Q[i] - a[4 + i] - br;
+      a[4 + i] = (uint64_t)d;
+      br = (d >> 64) & 1;
+    }
+  }
+  std::vector<uint64_t> in(4 * inputs.size());
+  for (size_t i = 0; i < inputs.size(); i++) memcpy(&in[4 * i], inputs[i].data(), 32);
+  int ok = 0;
+  if (zkmi_groth16_verify(vk_.data(), vk_.size(), in.data(), inputs.size(), a, b, c, &ok) != 0)
+    fail("Failed to verify proof");
+  return ok == 1;
 }
 
 bool Groth16Prover::verify(const BatchProof& proof) const {

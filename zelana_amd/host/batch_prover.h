@@ -18,6 +18,7 @@
 
 #include <array>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <variant>
@@ -109,6 +110,10 @@ class Groth16Prover : public BatchProver {
 
   BatchProof prove(const BatchPublicInputs& inputs, const BatchWitness& witness) const override;
   bool verify(const BatchProof& proof) const override;  // length check, as the reference (:427-442)
+  // The on-chain verifier's pairing check (verifier lib.rs:497-547) on the
+  // host, under this prover's VK: `inputs` = the circuit's 7 instance values
+  // (canonical 4 x u64 each); proof.proof_bytes = the 256-B layout of prove().
+  bool verify_pairing(const BatchProof& proof, const std::vector<std::array<uint64_t, 4>>& inputs) const;
   Bytes32 verification_key_hash() const override { return vk_hash_; }
   const std::vector<uint8_t>& verifying_key() const { return vk_; }
   // -A || B || C, little-endian coordinates (prover.rs:304-334)
@@ -122,6 +127,9 @@ class Groth16Prover : public BatchProver {
   zkmi_pk* pk_ = nullptr;
   std::vector<uint8_t> vk_;
   Bytes32 vk_hash_{};
+  // BatchProver is shared (Arc<dyn BatchProver>: Send + Sync) but a zkmi
+  // context serves one call at a time (zkmi.h): prove() serialises on it
+  mutable std::mutex gpu_mu_;
 };
 
 // BLAKE3 compute_batch_hash over the transactions (prover.rs:525-558)

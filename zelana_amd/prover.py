@@ -185,6 +185,13 @@ class Groth16Prover:
         # reference semantics (prover.rs:427-442): length check only
         return len(proof.proof_bytes) == 256
 
+    def verify_pairing(self, proof: BatchProof, public_inputs) -> bool:
+        """The on-chain verifier's check (verifier lib.rs:497-547) on the host:
+        e(A,B) = e(alpha,beta) e(vk_x,gamma) e(C,delta) under this prover's VK
+        (zkmi_groth16_verify).  public_inputs: the circuit's instance values
+        (ints), without the leading One."""
+        return gpu.groth16_verify(self.verifying_key, public_inputs, proof.a, proof.b, proof.c)
+
     def verification_key_hash(self) -> bytes:
         return self.vk_hash
 
