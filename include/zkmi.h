@@ -239,6 +239,15 @@ void zkmi_r1cs_destroy(zkmi_r1cs_dev* cs);
 int zkmi_groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs_dev* cs, const void* d_z,
                                 const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
                                 uint64_t c_out[8]);
+/* Asynchronous form of the resident prove: submit queues the witness map and
+ * the five MSMs and returns; wait finishes the MSM epilogues and the
+ * assembly.  Several proofs may be in flight on one context (finish them in
+ * submission order); d_z must stay unchanged until its proof's wait returns,
+ * unless a zkmi_wprog_run writing it is ordered after (see there). */
+typedef struct zkmi_proof_job zkmi_proof_job;
+int zkmi_groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs_dev* cs, const void* d_z,
+                              const uint64_t r[4], const uint64_t s[4], zkmi_proof_job** job);
+int zkmi_groth16_prove_wait(zkmi_proof_job* job, uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]);
 /* Benchmark helper: a random proving key of domain 2^log_n with the given
  * instance/witness counts, generated in HBM.  Proofs made with it do not
  * verify; the proving work is identical to a real key of that shape. */
@@ -275,6 +284,42 @@ int zkmi_proof_to_solana_bytes(const uint64_t a[8], const uint64_t b[16], const 
 /* 128 B arkworks Proof::serialize_compressed (a 32 || b 64 || c 32) */
 int zkmi_proof_serialize_compressed(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8],
                                     uint8_t out[128]);
+
+/* ------------------------------------------------------ witness programs
+ * Per-batch witness generation on the GPU: a proving
+ * key fits one circuit shape, so a batch's full assignment z is a fixed
+ * straight-line program over Fr of its ~thousands of free inputs (for
+ * zelana_batch: Prover.toml's values; 99% of z is MiMC round values,
+ * prover-worker/src/mimc.rs:52-142).  The program is recorded once on the
+ * host (zelana_amd/wprog.py); per batch only the inputs travel, and z is
+ * written straight into HBM for zkmi_groth16_prove_resident.
+ *   op i: 4 x u32 {kind | a_len << 8 | b_len << 20, out, a_off, b_off};
+ *         kinds 1 MUL z[out] = <a,z><b,z>; 2 INV z[out] = <a,z>^-1 (0 -> 0);
+ *         3 BITS64 z[out+i] = bit i of <a,z>; 4 PERM MiMC permutation of
+ *         <a,z>: z[out + 4r + (0..3)] = t_r^2, t_r^4, t_r^6, t_r^7 (91 rounds,
+ *         t_0 = <a,z> + c_0, t_r = t_{r-1}^7 + c_r, c_i = (i+1)^3 + (i+1))
+ *   term: 2 x u32 {z index, coefficient index}; <a,z> = sum over
+ *         term[a_off .. a_off + a_len) of coeff * z
+ *   levels: ops [level_start[l], level_start[l+1]) depend only on inputs and
+ *         earlier levels. */
+typedef struct zkmi_wprog zkmi_wprog;
+typedef struct {
+  size_t num_vars;                             /* |z| */
+  size_t num_inputs; const uint32_t* input_var; /* z index of input k */
+  size_t num_ops; const uint32_t* op;           /* num_ops x 4 */
+  size_t num_terms; const uint32_t* term;       /* num_terms x 2 */
+  size_t num_coeffs; const uint64_t* coeff;     /* num_coeffs x 4, canonical Fr */
+  size_t num_levels; const uint32_t* level_start; /* num_levels + 1 */
+} zkmi_wprog_desc;
+int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* desc, zkmi_wprog** out);
+void zkmi_wprog_destroy(zkmi_wprog* prog);
+/* z (device, num_vars x 32 B) <- the program over `inputs` (num_inputs x 4
+ * u64 canonical; input 0 is One = 1).  Later work on the context (a proof
+ * over z) waits for it.  async = 1: returns after queueing on the program's
+ * own stream, which runs beside the context's earlier work (the previous
+ * proof); it then waits only for context work queued before the PREVIOUS
+ * run, so callers alternate two z buffers. */
+int zkmi_wprog_run(zkmi_ctx* ctx, zkmi_wprog* prog, const uint64_t* inputs, void* d_z, int async);
 
 /* ------------------------------------------------- verification / on-chain
  * Host code (no GPU needed).  The reference's Groth16Prover::verify is a

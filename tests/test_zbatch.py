@@ -129,3 +129,36 @@ def test_batch70_native_witness_equals_python(monkeypatch):
     _python_only(monkeypatch)
     _, zp, cp = Z.build(d, witness_only=True)
     assert cn == cp and np.array_equal(zn, zp)
+
+
+@pytest.mark.parametrize("depth,ntx", [(2, 1), (3, 2)])
+def test_witness_program_plan(depth, ntx):
+    """The recorded witness program (zelana_amd/wprog.py, run on the GPU by
+    zkmi_wprog_run) reproduces build()'s z on the host interpreter, for the
+    template batch and for a different batch through zbatch.batch_inputs."""
+    from zelana_amd import wprog as W
+    kw = dict(max_transfers=ntx, max_withdrawals=1, max_shielded=1, depth=depth)
+    d = Z.synthetic_batch(depth, ntx, seed=100 + depth)
+    plan, cs, z = W.record(d, **kw)
+    inp = Z.batch_inputs(d, **kw)
+    rec = np.array([[(v >> (64 * k)) & ((1 << 64) - 1) for k in range(4)] for v in plan.template_inputs], np.uint64)
+    assert np.array_equal(inp, rec)
+    assert np.array_equal(plan.interpret(inp), z)
+    d2 = Z.synthetic_batch(depth, ntx, seed=7 + depth)
+    _, z2, _ = Z.build(d2, witness_only=True, **kw)
+    assert np.array_equal(plan.interpret(Z.batch_inputs(d2, **kw)), z2)
+    st = plan.stats()
+    assert st["ops"] == plan.op.shape[0] and st["levels"] == len(plan.level_start) - 1
+
+
+def test_batch_inputs_match_recording_full():
+    """batch 70 (the full circuit): the extractor's 1,695 inputs are exactly
+    the values the recording Builder saw, in order."""
+    from zelana_amd import wprog as W
+    d = Z.load_prover_toml(os.path.join(GOLD, "zelana_batch_70_Prover.toml"))
+    plan, _, _ = W.record(d)
+    inp = Z.batch_inputs(d)
+    rec = np.array([[(v >> (64 * k)) & ((1 << 64) - 1) for k in range(4)] for v in plan.template_inputs], np.uint64)
+    assert np.array_equal(inp, rec)
+    st = plan.stats()
+    assert st["vars"] == 1416759 and st["permutations"] > 3800

@@ -23,6 +23,14 @@ u8p = ctypes.POINTER(ctypes.c_uint8)
 sz = ctypes.c_size_t
 
 
+class WprogDesc(ctypes.Structure):
+    _fields_ = [
+        ("num_vars", sz), ("num_inputs", sz), ("input_var", vp), ("num_ops", sz), ("op", vp),
+        ("num_terms", sz), ("term", vp), ("num_coeffs", sz), ("coeff", vp), ("num_levels", sz),
+        ("level_start", vp),
+    ]
+
+
 class R1CSStruct(ctypes.Structure):
     _fields_ = [
         ("num_constraints", sz), ("num_instance", sz), ("num_witness", sz),
@@ -91,10 +99,15 @@ SIGNATURES = [
     ("zkmi_r1cs_create", ctypes.c_int, [vp, ctypes.POINTER(R1CSStruct), ctypes.POINTER(vp)]),
     ("zkmi_r1cs_destroy", None, [vp]),
     ("zkmi_groth16_prove_resident", ctypes.c_int, [vp, vp, vp, vp, u64p, u64p, u64p, u64p, u64p]),
+    ("zkmi_groth16_prove_submit", ctypes.c_int, [vp, vp, vp, vp, u64p, u64p, ctypes.POINTER(vp)]),
+    ("zkmi_groth16_prove_wait", ctypes.c_int, [vp, u64p, u64p, u64p]),
     ("zkmi_pk_synthetic", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint32, sz, sz, ctypes.POINTER(vp)]),
     ("zkmi_groth16_setup", ctypes.c_int, [vp, vp, u64p, u64p, u64p, ctypes.POINTER(vp)]),
     ("zkmi_pk_serialize", ctypes.c_int, [vp, u8p, sz, ctypes.POINTER(sz)]),
     ("zkmi_vk_canonical", ctypes.c_int, [vp, u8p, sz, u8p, sz, ctypes.POINTER(sz)]),
+    ("zkmi_wprog_create", ctypes.c_int, [vp, ctypes.POINTER(WprogDesc), ctypes.POINTER(vp)]),
+    ("zkmi_wprog_destroy", None, [vp]),
+    ("zkmi_wprog_run", ctypes.c_int, [vp, vp, u64p, vp, ctypes.c_int]),
     ("zkmi_groth16_verify", ctypes.c_int, [u8p, sz, u64p, sz, u64p, u64p, u64p, ctypes.POINTER(ctypes.c_int)]),
     ("zkmi_alt_bn128_pairing", ctypes.c_int, [u8p, sz, u8p]),
     ("zkmi_alt_bn128_g1_add", ctypes.c_int, [u8p, u8p]),

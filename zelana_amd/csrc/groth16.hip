@@ -775,11 +775,25 @@ int pk_compact_b(zkmi_pk* pk) {
   return 0;
 }
 
+}  // namespace zk
+
+// A proof in flight: its five MSM jobs are queued; wait finishes their host
+// epilogues and assembles A, B, C (ark-groth16 create_proof_with_assignment).
+struct zkmi_proof_job {
+  const zkmi_pk* pk;
+  zkmi_msm_job* jobs[5];  // h, l, a, b_g1, b_g2
+  uint64_t r[4], s[4];
+};
+
+namespace zk {
+
 // ------------------------------------------------------------ prove
-// core: R1CS and full assignment z already resident in HBM
-int groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
-                           const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
-                           uint64_t c_out[8]) {
+// core: R1CS and full assignment z already resident in HBM.  submit queues
+// everything (the witness map on the context stream, the MSMs on the lanes)
+// and returns; several proofs may be in flight, finished in order by wait.
+int groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
+                         const uint64_t r[4], const uint64_t s[4], zkmi_proof_job** out) {
+  *out = nullptr;
   size_t l = dr.l, w = dr.w, nv = l + w;
   uint32_t logn = domain_log(dr.m + l);
   if (l != pk->num_instance || w != pk->num_witness || ((size_t)1 << logn) != pk->n) {
@@ -796,8 +810,12 @@ int groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, 
   // lanes first, the witness map then runs on the context stream beside them
   // (filling their latency-bound sort / bucket-reduction phases), and the h
   // MSM follows it.  Each host epilogue overlaps later kernels.
-  zkmi_msm_job* jobs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  uint64_t h_acc[8], l_acc[8], a_acc[8], b1_acc[8], b2_acc[16];
+  zkmi_proof_job* pj = new zkmi_proof_job;
+  pj->pk = pk;
+  memcpy(pj->r, r, 32);
+  memcpy(pj->s, s, 32);
+  zkmi_msm_job** jobs = pj->jobs;
+  for (int i = 0; i < 5; i++) jobs[i] = nullptr;
   int rc = 0;
   rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
   if (!rc && pk->d_bidx) {  // a over z[1..V]; b1 / b2 over the compacted B variables
@@ -816,17 +834,41 @@ int groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, 
   }
   if (!rc) rc = witness_map_dev(ctx, dr, dz, logn, dh);
   if (!rc) rc = msm_submit(ctx, pk->h_query_rev, 0, dh, n - 1, &jobs[0]);
+  if (rc) {
+    for (auto* j : pj->jobs)
+      if (j) msm_job_free(j);
+    delete pj;
+    return rc;
+  }
+  *out = pj;
+  return 0;
+}
+
+int groth16_prove_wait(zkmi_proof_job* pj, uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]) {
+  const zkmi_pk* pk = pj->pk;
+  zkmi_msm_job** jobs = pj->jobs;
+  uint64_t h_acc[8], l_acc[8], a_acc[8], b1_acc[8], b2_acc[16];
+  int rc = 0;
   if (!rc) rc = msm_wait(jobs[1], l_acc), jobs[1] = nullptr;
   if (!rc) rc = msm_wait(jobs[2], a_acc), jobs[2] = nullptr;
   if (!rc) rc = msm_wait(jobs[3], b1_acc), jobs[3] = nullptr;
   if (!rc) rc = msm_wait(jobs[4], b2_acc), jobs[4] = nullptr;
   if (!rc) rc = msm_wait(jobs[0], h_acc), jobs[0] = nullptr;
-  for (auto* j : jobs)
-    if (j) msm_job_free(j);
-  if (rc) return rc;
-  groth16_assemble(pk->alpha_g1, pk->beta_g1, pk->delta_g1, pk->beta_g2, pk->delta_g2, pk->a0, pk->b1_0, pk->b2_0,
-                   h_acc, l_acc, a_acc, b1_acc, b2_acc, r, s, a_out, b_out, c_out);
-  return 0;
+  for (int i = 0; i < 5; i++)
+    if (jobs[i]) msm_job_free(jobs[i]);
+  if (!rc)
+    groth16_assemble(pk->alpha_g1, pk->beta_g1, pk->delta_g1, pk->beta_g2, pk->delta_g2, pk->a0, pk->b1_0, pk->b2_0,
+                     h_acc, l_acc, a_acc, b1_acc, b2_acc, pj->r, pj->s, a_out, b_out, c_out);
+  delete pj;
+  return rc;
+}
+
+int groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
+                           const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
+                           uint64_t c_out[8]) {
+  zkmi_proof_job* pj = nullptr;
+  ZK_TRY(groth16_prove_submit(ctx, pk, dr, dz, r, s, &pj));
+  return groth16_prove_wait(pj, a_out, b_out, c_out);
 }
 
 int groth16_prove(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs* cs, const uint64_t* z, const uint64_t r[4],
@@ -1298,6 +1340,26 @@ int zkmi_groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1c
   }
   int rc = groth16_prove_resident(ctx, pk, *cs, (const uint32_t*)d_z, r, s, a_out, b_out, c_out);
   if (rc == 0) rc = timer_flush(ctx);
+  return rc;
+}
+int zkmi_groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs_dev* cs, const void* d_z,
+                              const uint64_t r[4], const uint64_t s[4], zkmi_proof_job** job) {
+  ZK_DEVICE_GUARD(ctx);
+  if (!ctx || !pk || !cs || !d_z || !r || !s || !job) {
+    set_error("zkmi_groth16_prove_submit: null argument");
+    return ZKMI_EINVAL;
+  }
+  return groth16_prove_submit(ctx, pk, *cs, (const uint32_t*)d_z, r, s, job);
+}
+int zkmi_groth16_prove_wait(zkmi_proof_job* job, uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]) {
+  if (!job || !a_out || !b_out || !c_out) {
+    set_error("zkmi_groth16_prove_wait: null argument");
+    return ZKMI_EINVAL;
+  }
+  zkmi_ctx* ctx = job->pk->ctx;
+  ZK_DEVICE_GUARD(ctx);
+  int rc = groth16_prove_wait(job, a_out, b_out, c_out);
+  if (rc == 0) rc = timer_flush(ctx, false);
   return rc;
 }
 int zkmi_pk_synthetic(zkmi_ctx* ctx, uint64_t seed, uint32_t log_n, size_t num_instance, size_t num_witness,

@@ -1,0 +1,536 @@
+// wprog.hip — witness programs: per-batch witness generation on the GPU,
+// writing the full assignment z straight into HBM.
+//
+// The zelana_batch circuit (forge/circuits/zelana_batch/src/main.nr) is 99%
+// MiMC: ~3,900 permutations of 91 rounds x -> (x + c_i)^7 whose per-round
+// values t^2, t^4, t^6, t^7 are the witness (host restatement
+// prover-worker/src/mimc.rs:52-142; zelana_amd/zbatch.py).  Its proving key
+// fits one circuit shape, so the witness is a FIXED straight-line program over
+// Fr; only ~2,400 free inputs (Prover.toml values) change per batch.  The
+// program is recorded once on the host (zelana_amd/wprog.py) as ops over
+// linear combinations of z, grouped into dependency levels:
+//   MUL    z[out] = <a, z> * <b, z>                (products, selects, Merkle d)
+//   INV    z[out] = <a, z>^-1 or 0                 (signature != 0 witnesses)
+//   BITS64 z[out + i] = bit i of <a, z>, i < 64    (u64 range checks)
+//   PERM   z[out + 4 r + k] = (t_r^2, t_r^4, t_r^6, t_r^7), t_0 = <a, z> + c_0,
+//          t_r = t_{r-1}^7 + c_r                   (one MiMC permutation)
+// and each level is one launch; a batch uploads only its inputs.
+//
+// The program is latency-bound, not throughput-bound: its critical path is
+// ~70 dependent permutations (a depth-32 Merkle path is 64 of them) with ~57
+// independent chains beside it, so one launch holds a wave or two.  A
+// permutation is therefore worked by a QUAD of lanes: all four square t, two
+// pairs form t^4 / t^3 and then t^6 / t^7 (DPP quad broadcasts exchange
+// them), and each lane converts and stores one of the round's four values
+// (the four stores of a round are one 128-byte run).  That keeps the
+// dependent chain per round at three Montgomery products.  The witness stream
+// runs beside the previous batch's proof (zkmi_wprog_run, async): it occupies
+// a few CUs while the prover has the rest.
+//
+// Column chains are left to the compiler here (ZK_NO_ASM_MAD): with one wave
+// per SIMD, the mad latency it hides by splitting columns matters more than
+// the add it costs (the opposite trade of the throughput kernels).
+#define ZK_NO_ASM_MAD 1
+#include <string.h>
+
+#include <vector>
+
+#include "dev_io.h"
+#include "ff.h"
+#include "zkmi_internal.h"
+
+namespace zk {
+
+constexpr int WP_MUL = 1, WP_INV = 2, WP_BITS64 = 3, WP_PERM = 4;
+constexpr int MIMC_R = 91;
+
+// a * 2^-261 mod r for a < 2^261 with normalised limbs: Montgomery reduction
+// alone (a product with 1 without its 81 product mads)
+__device__ __forceinline__ Fe redc_fr(const Fe& a) {
+  uint32_t m[NL];
+  Fe r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    acc += a.v[k];
+#pragma unroll
+    for (int j = 0; j < k; j++) acc += (uint64_t)m[j] * FrP::P[k - j];
+    m[k] = ((uint32_t)acc * FrP::PINV) & LMASK;
+    acc += (uint64_t)m[k] * FrP::P[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) acc += (uint64_t)m[j] * FrP::P[k - j];
+    r.v[k - NL] = (uint32_t)acc & LMASK;
+    acc >>= 29;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+// Montgomery product (R = 2^261, lazy: < 2p out) with four independent
+// accumulators per product-scanning column (even / odd j for the a*b and the
+// m*p terms): one wave per SIMD exposes the mad latency of a single chain,
+// and splitting it cuts the dependent chain per column to ~k/2 mads.
+__device__ __forceinline__ Fe mul_ilp(const Fe& a, const Fe& b) {
+  uint32_t m[NL];
+  Fe r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    uint64_t s0 = c, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      if (j & 1) {
+        s1 += (uint64_t)a.v[j] * b.v[k - j];
+        s3 += (uint64_t)m[j] * FrP::P[k - j];
+      } else {
+        s0 += (uint64_t)a.v[j] * b.v[k - j];
+        s2 += (uint64_t)m[j] * FrP::P[k - j];
+      }
+    }
+    if (k & 1) s1 += (uint64_t)a.v[k] * b.v[0];
+    else s0 += (uint64_t)a.v[k] * b.v[0];
+    uint64_t tot = (s0 + s1) + (s2 + s3);
+    m[k] = ((uint32_t)tot * FrP::PINV) & LMASK;
+    tot += (uint64_t)m[k] * FrP::P[0];
+    c = tot >> 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+    uint64_t s0 = c, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) {
+      if (j & 1) {
+        s1 += (uint64_t)a.v[j] * b.v[k - j];
+        s3 += (uint64_t)m[j] * FrP::P[k - j];
+      } else {
+        s0 += (uint64_t)a.v[j] * b.v[k - j];
+        s2 += (uint64_t)m[j] * FrP::P[k - j];
+      }
+    }
+    const uint64_t tot = (s0 + s1) + (s2 + s3);
+    r.v[k - NL] = (uint32_t)tot & LMASK;
+    c = tot >> 29;
+  }
+  r.v[NL - 1] = (uint32_t)c;
+  return r;
+}
+
+// squaring with the same split: off-diagonal products once (doubled operand)
+__device__ __forceinline__ Fe sqr_ilp(const Fe& a) {
+  uint32_t m[NL], d[NL];
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) d[i] = a.v[i] << 1;
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    uint64_t s0 = c, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int j = 0; j < (k + 1) / 2; j++) {
+      if (j & 1) s1 += (uint64_t)d[j] * a.v[k - j];
+      else s0 += (uint64_t)d[j] * a.v[k - j];
+    }
+    if ((k & 1) == 0) s1 += (uint64_t)a.v[k / 2] * a.v[k / 2];
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      if (j & 1) s3 += (uint64_t)m[j] * FrP::P[k - j];
+      else s2 += (uint64_t)m[j] * FrP::P[k - j];
+    }
+    uint64_t tot = (s0 + s1) + (s2 + s3);
+    m[k] = ((uint32_t)tot * FrP::PINV) & LMASK;
+    tot += (uint64_t)m[k] * FrP::P[0];
+    c = tot >> 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+    uint64_t s0 = c, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) {
+      if (j & 1) s1 += (uint64_t)d[j] * a.v[k - j];
+      else s0 += (uint64_t)d[j] * a.v[k - j];
+    }
+    if ((k & 1) == 0) s1 += (uint64_t)a.v[k / 2] * a.v[k / 2];
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) {
+      if (j & 1) s3 += (uint64_t)m[j] * FrP::P[k - j];
+      else s2 += (uint64_t)m[j] * FrP::P[k - j];
+    }
+    const uint64_t tot = (s0 + s1) + (s2 + s3);
+    r.v[k - NL] = (uint32_t)tot & LMASK;
+    c = tot >> 29;
+  }
+  r.v[NL - 1] = (uint32_t)c;
+  return r;
+}
+
+__device__ __forceinline__ void st_canon(uint32_t* z, uint32_t var, const Fe& v) {
+  uint32_t w[8];
+  pack(w, reduce<FrP>(v));
+  uint4* p = reinterpret_cast<uint4*>(z + (size_t)var * 8);
+  p[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  p[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+__device__ __forceinline__ Fe ld_canon(const uint32_t* z, uint32_t var) {
+  const uint4* p = reinterpret_cast<const uint4*>(z + (size_t)var * 8);
+  uint4 a = p[0], b = p[1];
+  uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return unpack(w);
+}
+
+// <terms, z>: coefficients held in Montgomery form, z canonical, so each
+// product mul(c R, x) = c x lands in value form (< 2p), summed mod 2p
+// (terms fetched four at a time so their loads are in flight together: a
+// dependent load chain per term costs microseconds on the short levels)
+__device__ __forceinline__ Fe eval_lc(const uint2* __restrict__ terms, uint32_t off, uint32_t len,
+                                      const uint32_t* __restrict__ coeff_m, const uint32_t* __restrict__ z) {
+  Fe acc = fe_zero();
+  uint32_t i = 0;
+  for (; i + 4 <= len; i += 4) {
+    uint2 t[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) t[k] = terms[off + i + k];
+    Fe c[4], x[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      c[k] = ld_canon(coeff_m, t[k].y);  // packed Montgomery coefficient
+      x[k] = ld_canon(z, t[k].x);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) acc = add<FrP>(acc, mul_ilp(c[k], x[k]));
+  }
+  for (; i < len; i++) {
+    const uint2 t = terms[off + i];
+    acc = add<FrP>(acc, mul_ilp(ld_canon(coeff_m, t.y), ld_canon(z, t.x)));
+  }
+  return acc;
+}
+__device__ __forceinline__ void st_raw(uint32_t* z, uint32_t var, const Fe& v) {
+  uint32_t w[8];
+  pack(w, v);
+  uint4* p = reinterpret_cast<uint4*>(z + (size_t)var * 8);
+  p[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  p[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+template <int LANE>
+__device__ __forceinline__ Fe quad_bcast(const Fe& x) {
+  constexpr int ctrl = LANE | (LANE << 2) | (LANE << 4) | (LANE << 6);  // quad_perm [L, L, L, L]
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.v[i], ctrl, 0xF, 0xF, false);
+  return r;
+}
+__device__ __forceinline__ Fe sel(bool c, const Fe& a, const Fe& b) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+// One level: op = lo + thread / 4, q = lane in its quad.  The four lanes of a
+// quad share an op, so a quad is either wholly active or wholly not (DPP
+// reads stay inside active quads).
+__global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ ops, uint32_t lo, uint32_t hi,
+                                                     const uint2* __restrict__ terms,
+                                                     const uint32_t* __restrict__ coeff_m,
+                                                     const uint32_t* __restrict__ rc_m, uint32_t* __restrict__ z) {
+  // Round constants in LDS: a global load inside the round loop would make
+  // every round wait (vmcnt) for the previous round's stores to land.
+  __shared__ uint32_t rc_s[MIMC_R * 8];
+  for (uint32_t i = threadIdx.x; i < MIMC_R * 8; i += blockDim.x) rc_s[i] = rc_m[i];
+  __syncthreads();
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t op_i = lo + (t >> 2), q = t & 3;
+  if (op_i >= hi) return;
+  const uint4 op = ops[op_i];
+  const int kind = op.x & 0xFF;
+  const uint32_t alen = (op.x >> 8) & 0xFFF, blen = op.x >> 20, out = op.y;
+  const Fe a = eval_lc(terms, op.z, alen, coeff_m, z);
+  if (kind == WP_PERM) {
+    const Fe r2 = fe_const<FrP>(FrP::R2);
+    Fe x = mul<FrP>(a, r2);  // Montgomery form
+    const bool odd = q & 1;
+    for (int r = 0; r < MIMC_R; r++) {
+      const Fe tm = add<FrP>(x, unpack(rc_s + 8 * r));
+      const Fe t2 = sqr_ilp(tm);
+      const Fe p = mul_ilp(t2, sel(odd, tm, t2));  // even lanes: t^4, odd: t^3
+      const Fe t4 = quad_bcast<0>(p), t3 = quad_bcast<1>(p);
+      const Fe u = mul_ilp(t4, sel(odd, t3, t2));  // even lanes: t^6, odd: t^7
+      x = quad_bcast<1>(u);                          // t^7 for the next round
+      const Fe mine = q == 0 ? t2 : (q == 1 ? t4 : u);  // lanes store t^2, t^4, t^6, t^7
+      // Montgomery form as is (k_wprog_canon converts them all afterwards in
+      // one wide pass), except the permutation's output, which later ops read
+      if (r == MIMC_R - 1 && q == 3) st_canon(z, out + 4 * (uint32_t)r + q, redc_fr(mine));
+      else st_raw(z, out + 4 * (uint32_t)r + q, mine);
+    }
+    return;
+  }
+  if (kind == WP_BITS64) {
+    uint32_t w[8];
+    pack(w, reduce<FrP>(a));
+    for (uint32_t i = q; i < 64; i += 4) {
+      Fe b = fe_zero();
+      b.v[0] = (w[i >> 5] >> (i & 31)) & 1;
+      st_canon(z, out + i, b);
+    }
+    return;
+  }
+  if (q != 0) return;
+  if (kind == WP_MUL) {
+    const Fe b = eval_lc(terms, op.w, blen, coeff_m, z);
+    st_canon(z, out, mul<FrP>(mul<FrP>(a, fe_const<FrP>(FrP::R2)), b));
+  } else if (kind == WP_INV) {
+    // r - 2 (Fermat); 0 stays 0
+    const uint64_t e[4] = {0x43e1f593efffffffULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL,
+                           0x30644e72e131a029ULL};
+    const Fe am = mul<FrP>(a, fe_const<FrP>(FrP::R2));
+    st_canon(z, out, redc_fr(reduce<FrP>(pow<FrP>(am, e))));
+  }
+}
+
+// Montgomery -> canonical for the first 4*91 - 1 trace values of every
+// permutation (the last one, its output, is stored canonical)
+__global__ void __launch_bounds__(256) k_wprog_canon(const uint32_t* __restrict__ perm_out, uint32_t nperm,
+                                                     uint32_t* __restrict__ z) {
+  constexpr uint32_t PER = 4 * MIMC_R - 1;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nperm * PER) return;
+  const uint32_t var = perm_out[i / PER] + i % PER;
+  st_canon(z, var, redc_fr(ld_canon(z, var)));
+}
+
+__global__ void __launch_bounds__(256) k_wprog_inputs(const uint32_t* __restrict__ in, const uint32_t* __restrict__ var,
+                                                      uint32_t n, uint32_t* __restrict__ z) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4* s = reinterpret_cast<const uint4*>(in + (size_t)i * 8);
+  uint4* d = reinterpret_cast<uint4*>(z + (size_t)var[i] * 8);
+  d[0] = s[0];
+  d[1] = s[1];
+}
+
+// canonical -> packed Montgomery (R = 2^261)
+__global__ void __launch_bounds__(256) k_wprog_to_mont(uint32_t* __restrict__ v, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8];
+  for (int k = 0; k < 8; k++) w[k] = v[(size_t)i * 8 + k];
+  pack(w, reduce<FrP>(mul<FrP>(unpack(w), fe_const<FrP>(FrP::R2))));
+  for (int k = 0; k < 8; k++) v[(size_t)i * 8 + k] = w[k];
+}
+
+}  // namespace zk
+
+struct zkmi_wprog {
+  zkmi_ctx* ctx = nullptr;
+  size_t num_vars = 0, num_inputs = 0;
+  uint32_t *d_input_var = nullptr, *d_coeff = nullptr, *d_rc = nullptr, *d_in = nullptr;
+  uint4* d_ops = nullptr;
+  uint2* d_terms = nullptr;
+  uint32_t* d_perm_out = nullptr;  // first trace variable of every permutation
+  uint32_t num_perms = 0;
+  std::vector<uint32_t> level_start;  // host: op ranges per level
+  std::vector<uint32_t> op_kinds;     // host: kinds (level geometry)
+  hipStream_t st = nullptr;           // the witness stream
+  hipEvent_t done = nullptr, ctx_mark = nullptr;
+  bool have_mark = false;
+  uint64_t* h_in[2] = {nullptr, nullptr};  // pinned staging of the inputs (alternating)
+  hipEvent_t in_done[2] = {nullptr, nullptr};
+  int next_in = 0;
+};
+
+namespace zk {
+static void wprog_free(zkmi_wprog* p) {
+  if (!p) return;
+  if (p->st) (void)hipStreamSynchronize(p->st);
+  (void)hipFree(p->d_input_var);
+  (void)hipFree(p->d_coeff);
+  (void)hipFree(p->d_rc);
+  (void)hipFree(p->d_in);
+  (void)hipFree(p->d_ops);
+  (void)hipFree(p->d_terms);
+  (void)hipFree(p->d_perm_out);
+  for (int b = 0; b < 2; b++) {
+    if (p->h_in[b]) (void)hipHostFree(p->h_in[b]);
+    if (p->in_done[b]) (void)hipEventDestroy(p->in_done[b]);
+  }
+  if (p->done) (void)hipEventDestroy(p->done);
+  if (p->ctx_mark) (void)hipEventDestroy(p->ctx_mark);
+  if (p->st) (void)hipStreamDestroy(p->st);
+  delete p;
+}
+}  // namespace zk
+
+using namespace zk;
+
+extern "C" {
+
+int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* d, zkmi_wprog** out) {
+  ZK_DEVICE_GUARD(ctx);
+  if (!ctx || !d || !out || !d->num_vars || !d->num_inputs || !d->input_var || (d->num_ops && !d->op) ||
+      !d->level_start || !d->num_coeffs || !d->coeff) {
+    set_error("zkmi_wprog_create: bad arguments");
+    return ZKMI_EINVAL;
+  }
+  // validate on the host: every index in range, levels cover the ops
+  if (d->level_start[0] != 0 || d->level_start[d->num_levels] != d->num_ops) {
+    set_error("zkmi_wprog_create: levels do not cover the ops");
+    return ZKMI_EINVAL;
+  }
+  for (size_t l = 0; l < d->num_levels; l++)
+    if (d->level_start[l] > d->level_start[l + 1]) {
+      set_error("zkmi_wprog_create: level starts not monotone");
+      return ZKMI_EINVAL;
+    }
+  for (size_t i = 0; i < d->num_inputs; i++)
+    if (d->input_var[i] >= d->num_vars) {
+      set_error("zkmi_wprog_create: input %zu outside z", i);
+      return ZKMI_EINVAL;
+    }
+  for (size_t i = 0; i < d->num_terms; i++)
+    if (d->term[2 * i] >= d->num_vars || d->term[2 * i + 1] >= d->num_coeffs) {
+      set_error("zkmi_wprog_create: term %zu out of range", i);
+      return ZKMI_EINVAL;
+    }
+  std::vector<uint32_t> kinds(d->num_ops);
+  for (size_t i = 0; i < d->num_ops; i++) {
+    const uint32_t* o = d->op + 4 * i;
+    const uint32_t kind = o[0] & 0xFF, alen = (o[0] >> 8) & 0xFFF, blen = o[0] >> 20;
+    const uint64_t span = kind == WP_PERM ? 4 * MIMC_R : kind == WP_BITS64 ? 64 : 1;
+    if (kind < WP_MUL || kind > WP_PERM || o[1] + span > d->num_vars || (uint64_t)o[2] + alen > d->num_terms ||
+        (uint64_t)o[3] + blen > d->num_terms || (kind != WP_MUL && blen)) {
+      set_error("zkmi_wprog_create: op %zu malformed", i);
+      return ZKMI_EINVAL;
+    }
+    kinds[i] = kind;
+  }
+  for (size_t i = 0; i < d->num_coeffs; i++) {
+    const uint64_t* c = d->coeff + 4 * i;
+    // < r (canonical)
+    const uint64_t R[4] = {0x43e1f593f0000001ULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL,
+                           0x30644e72e131a029ULL};
+    bool lt = false;
+    for (int k = 3; k >= 0; k--)
+      if (c[k] != R[k]) {
+        lt = c[k] < R[k];
+        break;
+      }
+    if (!lt) {
+      set_error("zkmi_wprog_create: coefficient %zu not reduced", i);
+      return ZKMI_EINVAL;
+    }
+  }
+  zkmi_wprog* p = new zkmi_wprog;
+  p->ctx = ctx;
+  p->num_vars = d->num_vars;
+  p->num_inputs = d->num_inputs;
+  p->level_start.assign(d->level_start, d->level_start + d->num_levels + 1);
+  p->op_kinds = kinds;
+  auto fail = [&](const char* what) {
+    (void)hipGetLastError();
+    set_error("zkmi_wprog_create: %s", what);
+    wprog_free(p);
+    return ZKMI_EHIP;
+  };
+  // Highest stream priority: the program is a chain of ~140 small launches
+  // that must get onto CUs between the blocks of the proof running beside it
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (hipStreamCreateWithPriority(&p->st, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipEventCreateWithFlags(&p->done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->ctx_mark, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->in_done[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&p->in_done[1], hipEventDisableTiming) != hipSuccess)
+    return fail("stream / events");
+  std::vector<uint32_t> perm_out;
+  for (size_t i = 0; i < d->num_ops; i++)
+    if (kinds[i] == WP_PERM) perm_out.push_back(d->op[4 * i + 1]);
+  p->num_perms = (uint32_t)perm_out.size();
+  const size_t ni = d->num_inputs, no = std::max<size_t>(1, d->num_ops), nt = std::max<size_t>(1, d->num_terms);
+  if (hipMalloc(&p->d_perm_out, std::max<size_t>(1, perm_out.size()) * 4) != hipSuccess ||
+      (!perm_out.empty() && hipMemcpy(p->d_perm_out, perm_out.data(), perm_out.size() * 4, hipMemcpyHostToDevice) !=
+                                hipSuccess))
+    return fail("permutation list");
+  if (hipMalloc(&p->d_input_var, ni * 4) != hipSuccess || hipMalloc(&p->d_in, ni * 32) != hipSuccess ||
+      hipMalloc(&p->d_ops, no * 16) != hipSuccess || hipMalloc(&p->d_terms, nt * 8) != hipSuccess ||
+      hipMalloc(&p->d_coeff, d->num_coeffs * 32) != hipSuccess || hipMalloc(&p->d_rc, MIMC_R * 32) != hipSuccess ||
+      hipHostMalloc(&p->h_in[0], ni * 32, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&p->h_in[1], ni * 32, hipHostMallocDefault) != hipSuccess)
+    return fail("allocation");
+  // MiMC round constants c_i = (i+1)^3 + (i+1) (poseidon.nr:15-56)
+  uint64_t rc[MIMC_R * 4] = {0};
+  for (int i = 0; i < MIMC_R; i++) rc[4 * i] = (uint64_t)(i + 1) * (i + 1) * (i + 1) + (i + 1);
+  hipStream_t st = p->st;
+  if (hipMemcpyAsync(p->d_input_var, d->input_var, ni * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+      (d->num_ops && hipMemcpyAsync(p->d_ops, d->op, d->num_ops * 16, hipMemcpyHostToDevice, st) != hipSuccess) ||
+      (d->num_terms && hipMemcpyAsync(p->d_terms, d->term, d->num_terms * 8, hipMemcpyHostToDevice, st) != hipSuccess) ||
+      hipMemcpyAsync(p->d_coeff, d->coeff, d->num_coeffs * 32, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(p->d_rc, rc, sizeof(rc), hipMemcpyHostToDevice, st) != hipSuccess)
+    return fail("upload");
+  k_wprog_to_mont<<<(unsigned)((d->num_coeffs + 255) / 256), 256, 0, st>>>(p->d_coeff, (uint32_t)d->num_coeffs);
+  k_wprog_to_mont<<<1, 256, 0, st>>>(p->d_rc, MIMC_R);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return fail("init kernels");
+  *out = p;
+  return 0;
+}
+
+void zkmi_wprog_destroy(zkmi_wprog* p) {
+  if (!p) return;
+  ZK_DEVICE_GUARD(p->ctx);
+  wprog_free(p);
+}
+
+int zkmi_wprog_run(zkmi_ctx* ctx, zkmi_wprog* p, const uint64_t* inputs, void* d_z, int async) {
+  ZK_DEVICE_GUARD(ctx);
+  if (!ctx || !p || !inputs || !d_z || p->ctx != ctx) {
+    set_error("zkmi_wprog_run: bad arguments");
+    return ZKMI_EINVAL;
+  }
+  hipStream_t st = p->st;
+  // The z this run writes was last read by context work enqueued before the
+  // previous run (callers alternate two z buffers): wait for exactly that,
+  // so this run overlaps the previous batch's proof.  Synchronous runs wait
+  // for the whole context first.
+  if (!async) ZK_TRY(ctx_sync_all(ctx));
+  const int b = p->next_in;
+  p->next_in ^= 1;
+  ZK_HIP(hipEventSynchronize(p->in_done[b]));  // that staging buffer's last upload has landed
+  memcpy(p->h_in[b], inputs, p->num_inputs * 32);
+  if (p->have_mark) ZK_HIP(hipStreamWaitEvent(st, p->ctx_mark, 0));
+  uint32_t* z = (uint32_t*)d_z;
+  ScopedKernelTimer tm(ctx, "wprog", st);
+  ZK_HIP(hipMemcpyAsync(p->d_in, p->h_in[b], p->num_inputs * 32, hipMemcpyHostToDevice, st));
+  ZK_HIP(hipEventRecord(p->in_done[b], st));
+  k_wprog_inputs<<<(unsigned)((p->num_inputs + 255) / 256), 256, 0, st>>>(p->d_in, p->d_input_var,
+                                                                        (uint32_t)p->num_inputs, z);
+  for (size_t l = 0; l + 1 < p->level_start.size(); l++) {
+    const uint32_t lo = p->level_start[l], hi = p->level_start[l + 1];
+    if (hi == lo) continue;
+    const size_t threads = (size_t)(hi - lo) * 4;
+    k_wprog_level<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(p->d_ops, lo, hi, p->d_terms, p->d_coeff,
+                                                                    p->d_rc, z);
+  }
+  if (p->num_perms) {
+    const size_t nconv = (size_t)p->num_perms * (4 * MIMC_R - 1);
+    k_wprog_canon<<<(unsigned)((nconv + 255) / 256), 256, 0, st>>>(p->d_perm_out, p->num_perms, z);
+  }
+  ZK_HIP(hipGetLastError());
+  ZK_HIP(hipEventRecord(p->done, st));
+  // later context work (the proof over this z) waits for the witness
+  ZK_HIP(hipStreamWaitEvent(ctx->stream, p->done, 0));  // MSM lanes fork from the context stream
+  // everything enqueued on the context so far (the previous proof, which
+  // reads the other z buffer) must finish before the NEXT run writes it
+  ZK_HIP(hipEventRecord(p->ctx_mark, ctx->stream));
+  p->have_mark = true;
+  if (!async) {
+    ZK_HIP(hipStreamSynchronize(st));
+    return timer_flush(ctx);
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -485,6 +485,20 @@ def synthetic_pk(ctx: Context, seed: int, log_n: int, num_instance: int, num_wit
     return pk
 
 
+def groth16_prove_submit(ctx: Context, pk: "ProvingKey", r1cs: R1CSDevice, dz: DeviceBuffer, r: int, s: int):
+    """Queue a resident proof (zkmi_groth16_prove_submit); finish with groth16_prove_wait."""
+    job = vp()
+    check(lib().zkmi_groth16_prove_submit(ctx.h, pk.h, r1cs.h, dz.ptr, _p64(_limbs(r)), _p64(_limbs(s)),
+                                          ctypes.byref(job)), "zkmi_groth16_prove_submit")
+    return job
+
+
+def groth16_prove_wait(job):
+    a, b, c = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+    check(lib().zkmi_groth16_prove_wait(job, _p64(a), _p64(b), _p64(c)), "zkmi_groth16_prove_wait")
+    return a, b, c
+
+
 def groth16_prove_resident(ctx: Context, pk: "ProvingKey", r1cs: R1CSDevice, dz: DeviceBuffer, r: int, s: int):
     a, b, c = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
     check(lib().zkmi_groth16_prove_resident(ctx.h, pk.h, r1cs.h, dz.ptr, _p64(_limbs(r)), _p64(_limbs(s)), _p64(a),

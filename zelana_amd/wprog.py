@@ -1,0 +1,199 @@
+"""Witness programs: per-batch witness generation on the GPU (zkmi_wprog_*).
+
+A proving key fits one circuit shape, so a batch's full assignment z is a
+fixed straight-line program over Fr of the batch's free inputs.  For the
+config-4 circuit (forge/circuits/zelana_batch, zelana_amd/zbatch.py) the
+program is recorded once by running zbatch.build with a recording Builder on a
+template batch; per batch, zbatch.batch_inputs() extracts the ~2.4K input
+values from a Prover.toml-shaped dict and libzkmi evaluates the program into
+z in HBM (wprog.hip), where zkmi_groth16_prove_resident reads it.  The host
+no longer builds the 1.42M-entry z, and z never crosses PCIe.
+
+Ops (zkmi.h "witness programs"): MUL, INV, BITS64, PERM (one MiMC
+permutation: 364 trace values), each over linear combinations of z, grouped
+into dependency levels (level = 1 + the deepest level among the variables an
+op reads; inputs are level 0).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import zbatch
+from ._lib import WprogDesc, check, lib, u64p, vp
+
+KINDS = {"mul": 1, "inv": 2, "bits64": 3, "perm": 4}
+SPAN = {"mul": 1, "inv": 1, "bits64": 64, "perm": 4 * zbatch.MIMC_ROUNDS}
+
+
+class Plan:
+    """Host-side witness program of one circuit shape (numpy arrays in the
+    layout zkmi_wprog_desc expects)."""
+
+    def __init__(self, b: "zbatch.Builder"):
+        assert b.record, "record with Builder(record=True)"
+        R = zbatch.R
+        nv = b.nv
+        self.num_vars = nv
+        self.num_instance = b.num_instance
+        self.input_var = np.array(b.input_vars, np.uint32)
+        self.template_inputs = np.array(b.input_vals, dtype=object)
+        produced = np.zeros(nv, bool)
+        produced[self.input_var] = True
+        coeffs: dict[int, int] = {}
+
+        def cid(c):
+            c %= R
+            i = coeffs.get(c)
+            if i is None:
+                i = coeffs[c] = len(coeffs)
+            return i
+
+        # Schedule by permutation depth: a permutation costs ~1000 times a
+        # MUL, so the launch sequence is [cheap sub-levels after stage S] then
+        # [permutation stage S + 1]: every permutation sits at its own chain's
+        # permutation depth (67 stages for zelana_batch) instead of at an op
+        # depth that counts the MULs between permutations (85 stages).
+        #   pstage(var): the permutation stage after which var exists
+        #   sub(var):    cheap sub-level after that stage (0 for perm outputs)
+        pstage = np.zeros(nv, np.int32)
+        sub = np.zeros(nv, np.int32)
+        BIG = 1 << 20
+        ops = []  # (key, kind, out, a_terms, b_terms)
+        for kind, out, at, bt in b.ops:
+            vs = [v for v, _ in list(at) + list(bt) if v]
+            s_in = max([int(pstage[v]) for v in vs] or [0])
+            span = SPAN[kind]
+            assert not produced[out:out + span].any(), "variable written twice"
+            produced[out:out + span] = True
+            if kind == "perm":
+                st = s_in + 1
+                pstage[out:out + span] = st
+                sub[out:out + span] = 0
+                key = (st - 1, BIG)
+            else:
+                sl = 1 + max([int(sub[v]) for v in vs if pstage[v] == s_in] or [0])
+                pstage[out:out + span] = s_in
+                sub[out:out + span] = sl
+                key = (s_in, sl)
+            ops.append((key, KINDS[kind], out, at, bt))
+        missing = np.nonzero(~produced)[0]
+        assert missing.size == 0, f"{missing.size} variables neither inputs nor op outputs (first {missing[:5]})"
+        # within a level: permutations first (quads of one wave share a kind)
+        ops.sort(key=lambda o: (o[0], -o[1]))
+        terms, oparr = [], np.zeros((len(ops), 4), np.uint32)
+        for i, (lv, kind, out, at, bt) in enumerate(ops):
+            aoff = len(terms)
+            terms += [(v, cid(c)) for v, c in at]
+            boff = len(terms)
+            terms += [(v, cid(c)) for v, c in bt]
+            assert len(at) < 4096 and len(bt) < 4096
+            oparr[i] = (kind | (len(at) << 8) | (len(bt) << 20), out, aoff, boff)
+        self.op = oparr
+        self.term = np.array(terms, np.uint32).reshape(-1, 2) if terms else np.zeros((0, 2), np.uint32)
+        table = sorted(coeffs.items(), key=lambda kv: kv[1])
+        self.coeff = np.array([[(c >> (64 * k)) & 0xFFFFFFFFFFFFFFFF for k in range(4)] for c, _ in table],
+                              np.uint64).reshape(-1, 4)
+        keys = sorted(set(o[0] for o in ops))
+        kid = {k: i for i, k in enumerate(keys)}
+        lv = np.array([kid[o[0]] for o in ops], np.int64)
+        self.num_levels = len(keys)
+        starts = np.searchsorted(lv, np.arange(0, self.num_levels + 1))
+        self.level_start = starts.astype(np.uint32)
+        self.kinds = oparr[:, 0] & 0xFF
+        # permutation outputs (the kernel stores the first 363 trace values of
+        # each in Montgomery form; a final pass converts them)
+        self.perm_out = np.array([o[2] for o in ops if o[1] == KINDS["perm"]], np.uint32)
+
+    def stats(self) -> dict:
+        perm_levels = sum(1 for l in range(self.num_levels)
+                          if (self.kinds[self.level_start[l]:self.level_start[l + 1]] == KINDS["perm"]).any())
+        return {"vars": self.num_vars, "inputs": int(self.input_var.size), "ops": int(self.op.shape[0]),
+                "permutations": int((self.kinds == KINDS["perm"]).sum()), "levels": self.num_levels,
+                "levels_with_permutations": perm_levels, "terms": int(self.term.shape[0]),
+                "coefficients": int(self.coeff.shape[0])}
+
+    def interpret(self, inputs: np.ndarray) -> np.ndarray:
+        """Host evaluation of the program (test reference for small
+        circuits; MiMC traces from the native host library when built)."""
+        R = zbatch.R
+        z = [0] * self.num_vars
+        for var, row in zip(self.input_var, inputs):
+            z[int(var)] = zbatch._int(np.ascontiguousarray(row))
+
+        coeffs = [zbatch._int(np.ascontiguousarray(c)) for c in self.coeff]
+
+        def ev(off, n):
+            return sum(z[int(v)] * coeffs[int(c)] for v, c in self.term[off:off + n]) % R
+        for kind, out, aoff, boff in self.op.astype(np.int64):
+            k, alen, blen = kind & 0xFF, (kind >> 8) & 0xFFF, kind >> 20
+            a = ev(aoff, alen)
+            if k == KINDS["mul"]:
+                z[out] = a * ev(boff, blen) % R
+            elif k == KINDS["inv"]:
+                z[out] = pow(a, R - 2, R) if a else 0
+            elif k == KINDS["bits64"]:
+                for i in range(64):
+                    z[out + i] = (a >> i) & 1
+            else:
+                t = a
+                for r, c in enumerate(zbatch.RC):
+                    t = (t + c) % R
+                    t2 = t * t % R
+                    t4 = t2 * t2 % R
+                    t6 = t4 * t2 % R
+                    t7 = t6 * t % R
+                    z[out + 4 * r:out + 4 * r + 4] = [t2, t4, t6, t7]
+                    t = t7
+        raw = b"".join(v.to_bytes(32, "little") for v in z)
+        return np.frombuffer(raw, np.uint64).reshape(-1, 4).copy()
+
+
+def record(template: dict, **build_kw):
+    """Run zbatch.build once with a recording Builder: (plan, cs, z)."""
+    b = zbatch.Builder(record=True)
+    cs, z, _ = zbatch.build(template, builder=b, **build_kw)
+    return Plan(b), cs, z
+
+
+class WitnessProgram:
+    """A Plan resident on the GPU (zkmi_wprog_create)."""
+
+    def __init__(self, ctx, plan: Plan):
+        self.ctx, self.plan = ctx, plan
+        d = WprogDesc()
+        d.num_vars = plan.num_vars
+        d.num_inputs = plan.input_var.size
+        d.input_var = plan.input_var.ctypes.data
+        d.num_ops = plan.op.shape[0]
+        d.op = plan.op.ctypes.data
+        d.num_terms = plan.term.shape[0]
+        d.term = plan.term.ctypes.data
+        d.num_coeffs = plan.coeff.shape[0]
+        d.coeff = plan.coeff.ctypes.data
+        d.num_levels = plan.num_levels
+        d.level_start = plan.level_start.ctypes.data
+        self.h = vp()
+        check(lib().zkmi_wprog_create(ctx.h, ctypes.byref(d), ctypes.byref(self.h)), "zkmi_wprog_create")
+
+    def run(self, inputs: np.ndarray, dz, async_: bool = False):
+        """z (DeviceBuffer of num_vars x 32 B) <- the program over `inputs`
+        ((num_inputs, 4) canonical u64).  async_: queue beside the previous
+        proof (alternate two z buffers)."""
+        inp = np.ascontiguousarray(inputs, np.uint64)
+        assert inp.shape == (self.plan.input_var.size, 4), inp.shape
+        assert dz.nbytes >= self.plan.num_vars * 32
+        check(lib().zkmi_wprog_run(self.ctx.h, self.h, inp.ctypes.data_as(u64p), dz.ptr, int(async_)),
+              "zkmi_wprog_run")
+
+    def close(self):
+        if self.h:
+            lib().zkmi_wprog_destroy(self.h)
+            self.h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

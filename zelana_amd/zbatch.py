@@ -164,7 +164,7 @@ class Builder:
     constraints: MiMC permutations in bulk (identical 364-row shape), the rest
     as explicit rows."""
 
-    def __init__(self):
+    def __init__(self, record: bool = False):
         # values in variable order: lists of ints, and (4*91, 4) u64 arrays
         # for native MiMC traces; `vals` is the open int list
         self.vals = [1]
@@ -173,11 +173,25 @@ class Builder:
         self.num_instance = 1
         self.rows = {"a": [], "b": [], "c": []}
         self.perms = []  # (first variable, input terms)
+        # witness program (record=True): the free inputs (variables the batch
+        # supplies) and every derived witness as an op over linear
+        # combinations, in allocation order (zelana_amd/wprog.py)
+        self.record = record
+        self.input_vars = [0]  # z[0] = One is input 0
+        self.input_vals = [1]
+        self.ops = []  # (kind, out, a_terms, b_terms)
 
     # variables
     def instance(self, value: int) -> LC:
         assert self.nv == self.num_instance, "instance variables come first"
         self.num_instance += 1
+        return self.input(value)
+
+    def input(self, value: int) -> LC:
+        """A free input of the witness (a Prover.toml value), in order."""
+        if self.record:
+            self.input_vars.append(self.nv)
+            self.input_vals.append(value % R)
         return self.witness(value)
 
     def witness(self, value: int) -> LC:
@@ -207,6 +221,8 @@ class Builder:
             k, x = (a, b) if a.is_const() else (b, a)
             return LC([(var, c * k.v % R) for var, c in x.t if c * k.v % R], x.v * k.v)
         w = self.witness(a.v * b.v)
+        if self.record:
+            self.ops.append(("mul", w.t[0][0], a.t, b.t))
         self.enforce(a, b, w)
         return w
 
@@ -222,6 +238,8 @@ class Builder:
     def nonzero_if(self, pred: LC, x: LC):
         s = self.mul(pred, x)
         inv = self.witness(pow(s.v, R - 2, R) if s.v else 0)
+        if self.record:
+            self.ops.append(("inv", inv.t[0][0], s.t, []))
         self.enforce(s, inv, pred)
 
     def select(self, cond: LC, a: LC, b: LC) -> LC:
@@ -229,6 +247,8 @@ class Builder:
 
     def range64(self, x: LC):
         bits = [self.witness((x.v >> i) & 1) for i in range(64)]
+        if self.record:
+            self.ops.append(("bits64", bits[0].t[0][0], x.t, []))
         for bt in bits:
             self.boolean(bt)
         s = LC([(bt.t[0][0], 1 << i) for i, bt in enumerate(bits)], x.v)
@@ -238,6 +258,8 @@ class Builder:
         if x.is_const():
             return const(mimc_permute(x.v))
         v0 = self.nv
+        if self.record:
+            self.ops.append(("perm", v0, x.t, []))
         L = _native_mimc()
         if L is not None:
             tr = np.empty((4 * MIMC_ROUNDS, 4), np.uint64)
@@ -402,7 +424,8 @@ def _f(x) -> int:
 
 
 def build(prover: dict, max_transfers=MAX_TRANSFERS, max_withdrawals=MAX_WITHDRAWALS, max_shielded=MAX_SHIELDED,
-          public_from_witness: bool = False, depth: int = TREE_DEPTH, witness_only: bool = False):
+          public_from_witness: bool = False, depth: int = TREE_DEPTH, witness_only: bool = False,
+          builder: Builder | None = None):
     """R1CS + full assignment z for a Prover.toml-shaped dict (main.nr:112-357).
 
     public_from_witness: set the 7 public inputs to the values the witness
@@ -411,7 +434,7 @@ def build(prover: dict, max_transfers=MAX_TRANSFERS, max_withdrawals=MAX_WITHDRA
     Returns (cs, z, computed) with computed = the 7 recomputed public values.
     witness_only: skip the matrices (cs is None) — per-batch proving, where the
     circuit's R1CS (and its key) are fixed."""
-    b = Builder()
+    b = builder if builder is not None else Builder()
     pub = {k: b.instance(_f(prover.get(k, 0))) for k in PUBLIC}
     batch_id = pub["batch_id"]
     cur_root = pub["pre_state_root"]
@@ -420,7 +443,7 @@ def build(prover: dict, max_transfers=MAX_TRANSFERS, max_withdrawals=MAX_WITHDRA
     wd_acc = b.hash(const(5), batch_id)
 
     def w(x):
-        return b.witness(_f(x))
+        return b.input(_f(x))
 
     def path_vars(s, pre):
         path = [w(x) for x in list(s[pre + "_path"])[:depth]]
@@ -535,6 +558,49 @@ def build(prover: dict, max_transfers=MAX_TRANSFERS, max_withdrawals=MAX_WITHDRA
         return None, b.assignment(), computed
     cs, z = b.to_r1cs()
     return cs, z, computed
+
+
+def batch_inputs(prover: dict, max_transfers=MAX_TRANSFERS, max_withdrawals=MAX_WITHDRAWALS,
+                 max_shielded=MAX_SHIELDED, depth: int = TREE_DEPTH) -> np.ndarray:
+    """The free inputs of build()'s witness in allocation order (One, the 7
+    public inputs, then every w(...) of main.nr's slots): what a batch hands
+    the GPU witness program (zelana_amd/wprog.py) instead of the 1.4M-entry z.
+    Must follow build()'s order exactly (tests/test_zbatch.py checks it
+    against the recording Builder).  Returns (n_inputs, 4) canonical u64."""
+    vals = [1] + [_f(prover.get(k, 0)) for k in PUBLIC]
+
+    def path(s, pre):
+        vals.extend(_f(x) for x in list(s.get(pre + "_path", [0] * depth))[:depth])
+        vals.extend(_f(x) for x in list(s.get(pre + "_path_indices", [0] * depth))[:depth])
+
+    transfers = list(prover.get("transfers", []))[:max_transfers]
+    for i in range(max_transfers):
+        t = transfers[i] if i < len(transfers) else {}
+        vals += [_f(t.get("is_valid", False)), _f(t.get("sender_pubkey", 0)), _f(t.get("sender_balance", 0)),
+                 _f(t.get("sender_nonce", 0))]
+        path(t, "sender")
+        vals += [_f(t.get("receiver_pubkey", 0)), _f(t.get("receiver_balance", 0)), _f(t.get("receiver_nonce", 0))]
+        path(t, "receiver")
+        vals += [_f(t.get("amount", 0)), _f(t.get("signature", 0))]
+    withdrawals = list(prover.get("withdrawals", []))[:max_withdrawals]
+    for i in range(max_withdrawals):
+        t = withdrawals[i] if i < len(withdrawals) else {}
+        vals += [_f(t.get("is_valid", False)), _f(t.get("sender_pubkey", 0)), _f(t.get("sender_balance", 0)),
+                 _f(t.get("sender_nonce", 0))]
+        path(t, "sender")
+        vals += [_f(t.get("l1_recipient", 0)), _f(t.get("amount", 0)), _f(t.get("signature", 0))]
+    shielded = list(prover.get("shielded", []))[:max_shielded]
+    for i in range(max_shielded):
+        t = shielded[i] if i < len(shielded) else {}
+        vals += [_f(t.get(k, False if k in ("is_valid", "skip_verification") else 0))
+                 for k in ("is_valid", "skip_verification", "input_owner", "input_value", "input_blinding",
+                           "input_position")]
+        path(t, "input")
+        vals += [_f(t.get(k, 0)) for k in ("spending_key", "output_owner", "output_value", "output_blinding",
+                                           "output_commitment", "nullifier")]
+    vals += [_f(prover.get(k, 0)) for k in ("num_transfers", "num_withdrawals", "num_shielded")]
+    raw = b"".join(v.to_bytes(32, "little") for v in vals)
+    return np.frombuffer(raw, np.uint64).reshape(-1, 4).copy()
 
 
 def load_prover_toml(path: str) -> dict:
