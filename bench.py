@@ -38,7 +38,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_PEAK_G = 614.4  # G wave64 VALU instructions/s: 256 CU x 4 SIMD x 2.4 GHz / 4 cycles
 MSM_BYTES_PER_PAIR = 96  # 64 B affine G1 point + 32 B scalar
 NTT_BYTES_PER_ELEM = 64  # 32 B read + 32 B written per transform
 
@@ -238,14 +237,17 @@ def main():
     pmc = pmc_record(kernel, args.log_n)
     traffic = pmc.get("hbm_bytes")
     valu = None
-    if pmc.get("sq_insts_valu") and kcnt:
-        rate = pmc["sq_insts_valu"] / kavg_s
-        valu = {"bound": "valu", "achieved": round(rate / 1e9, 1), "peak": VALU_PEAK_G, "unit": "G wave-instr/s",
-                "frac": round(rate / 1e9 / VALU_PEAK_G, 4), "sq_insts_valu_per_launch": pmc["sq_insts_valu"],
-                "note": "the bound that applies: peak = 256 CU x 4 SIMD x 2.4 GHz / 4 cycles per wave64 VALU op "
-                        "(v_mad_u64_u32, which dominates, measured at that rate; gfx950 issues 32-bit ops in 2 "
-                        "cycles and clocks ~2.0 GHz under this load, see DESIGN.md); instructions from the "
-                        "committed profiles/pmc_traffic.json"}
+    if pmc.get("valu_issue_utilisation") is not None:
+        valu = {"bound": "valu", "kernel": kernel,
+                "issue_utilisation": pmc["valu_issue_utilisation"],
+                "sq_insts_valu_per_launch": pmc.get("sq_insts_valu"),
+                "achieved_G_wave_instr_per_s": round(pmc["sq_insts_valu"] / kavg_s / 1e9, 1)
+                if pmc.get("sq_insts_valu") and kcnt else None,
+                "pmc_clock_ghz": pmc.get("clock_ghz"),
+                "note": "the bound that applies: fraction of the 1024 SIMDs' cycles issuing VALU work, "
+                        "SQ_ACTIVE_INST_VALU x 4 / (1024 x GRBM_GUI_ACTIVE / 8), both counted on the same "
+                        "dispatches (no assumed clock or cycle cost); from the committed profiles/pmc_traffic.json "
+                        "(tools/profile_r02.sh, tools/pmc_r02.py)"}
     line = {
         "metric": "BN254 G1 MSM Mpoint-scalar/s + L2 proofs/sec at 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -394,6 +396,7 @@ def bench_ntt(ctx, log_n, world, sync_all, allmax, steps=5):
         if c:
             stages[k] = round(t / steps, 4)
     alg = NTT_BYTES_PER_ELEM * n * 2  # NTT + INTT
+    npmc = pmc_record("ntt_group", log_n)
     line = {
         "workload": f"Fr NTT + INTT 2^{log_n} (BASELINE.json configs[2]), natural order, device-resident"
                     + (f"; {world} replicas (one transform pair per GPU)" if world > 1 else ""),
@@ -404,6 +407,8 @@ def bench_ntt(ctx, log_n, world, sync_all, allmax, steps=5):
         "stage_ms": stages,
         "roundtrip_exact": roundtrip,
         "n_gpus": world,
+        "pmc_per_pass": {k: npmc.get(k) for k in ("hbm_bytes", "sq_insts_valu", "valu_issue_utilisation")
+                         if npmc.get(k) is not None} or None,
         "note": "VALU-bound (8 x 2^23 x 3 Montgomery butterflies); algorithmic bytes = 64 B/elem/transform; "
                 "achieved_GBs / frac_hbm per GPU",
     }

@@ -243,6 +243,10 @@ __global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ o
   __shared__ uint32_t rc_s[MIMC_R * 8];
   for (uint32_t i = threadIdx.x; i < MIMC_R * 8; i += blockDim.x) rc_s[i] = rc_m[i];
   __syncthreads();
+  // The program runs beside a proof whose MSM waves fill the same SIMDs:
+  // top wave priority wins the VALU arbitration for this latency-critical
+  // chain (a handful of waves against the proof's thousands)
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t op_i = lo + (t >> 2), q = t & 3;
   if (op_i >= hi) return;
