@@ -4,6 +4,8 @@ Bit-exact: MSM results are compared as canonical affine points (group law is
 exact), NTT outputs limb for limb.  Sizes keep the oracle within seconds;
 full-size (2^20 MSM, 2^24 NTT) checks use size-independent properties.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -300,3 +302,37 @@ def test_msm_items_path_2pow18(ctx):
         else:
             sc = _rand_scalars(np.random.default_rng(seed), n, "witness")
         assert np.array_equal(ctx.msm(b, sc), O.msm_g1(pts, sc, threads=16)), kind
+
+
+_BR_MODE2_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import oracle_ctypes as O
+from zelana_amd.gpu import Context
+ctx = Context(0)
+n = 3000
+rng = np.random.default_rng(7)
+for g2, c in ((False, 19), (False, 20), (False, 22), (True, 20)):
+    pts = O.gen_points_g2(90 + c, n // 2) if g2 else O.gen_points_g1(90 + c, n)
+    pts[3] = 0
+    b = ctx.bases_g2(pts) if g2 else ctx.bases_g1(pts)
+    b.precompute(c, 0)
+    m = len(pts)
+    sc = O.ints_to_array([int(x) for x in rng.integers(0, 2**62, m)]) if c == 22 else O.gen_scalars(c, m)
+    want = O.msm_g2(pts, sc) if g2 else O.msm_g1(pts, sc)
+    assert np.array_equal(ctx.msm(b, sc), want), (g2, c)
+print("ok")
+"""
+
+
+def test_bucket_reduction_mode2_subprocess():
+    """The opt-in fold + lines bucket reduction (ZKMI_BR_MODE=2, read once per
+    process, so it runs in a child) equals the oracle for G1 tables c = 19,
+    20, 22 and a G2 table c = 20."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, ZKMI_BR_MODE="2")
+    r = subprocess.run([sys.executable, "-c", _BR_MODE2_SCRIPT, os.path.dirname(here), here], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]

@@ -96,6 +96,15 @@ __device__ __forceinline__ void st_xyzz(uint32_t* p, const Xyzz<typename G::F>& 
   Io<F>::st(p + 3 * G::CW, v.zzz);
 }
 
+// Curve addition of the reductions (piece sums, cascade, bucket reduction).
+// (Split-column products for these 1-2 waves/SIMD kernels -- four independent
+// accumulators per column -- measured no faster: 2^20 lines kernel 217 -> 195
+// us, bit sums 139 -> 143 us; dropped.)
+template <class G>
+__device__ __forceinline__ Xyzz<typename G::F> br_add(const Xyzz<typename G::F>& p, const Xyzz<typename G::F>& q) {
+  return xyzz_add(p, q);
+}
+
 // ----------------------------------------------------------------- digits
 __host__ __device__ constexpr int msm_windows(int c) { return (254 + c - 1) / c + ((254 % c) == 0 ? 1 : 0); }
 
@@ -633,7 +642,7 @@ __global__ void __launch_bounds__(256) k_msm_cutsum(const uint32_t* __restrict__
   Xyzz<F> sum = ld_xyzz<G>(xpts + (size_t)(2 * t0 + 2) * XW);
   xvalid[2 * t0 + 2] = 0;
   for (uint32_t t = t0 + 1; t <= t1; t++) {
-    sum = xyzz_add(sum, ld_xyzz<G>(xpts + (size_t)(2 * t + 1) * XW));
+    sum = br_add<G>(sum, ld_xyzz<G>(xpts + (size_t)(2 * t + 1) * XW));
     xvalid[2 * t + 1] = 0;
   }
   st_xyzz<G>(buckets + (size_t)b * XW, sum);
@@ -1000,7 +1009,7 @@ __global__ void __launch_bounds__(256) k_items_combine(const uint32_t* __restric
   Xyzz<F> sum = ld_xyzz<G>(xpts + (size_t)s0 * XW);
   xvalid[s0] = 0;
   for (uint32_t q = 1; q < np; q++) {
-    sum = xyzz_add(sum, ld_xyzz<G>(xpts + (size_t)(s0 + q) * XW));
+    sum = br_add<G>(sum, ld_xyzz<G>(xpts + (size_t)(s0 + q) * XW));
     xvalid[s0 + q] = 0;
   }
   st_xyzz<G>(buckets + (size_t)b * XW, sum);
@@ -1046,7 +1055,7 @@ __global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ x
     }
     if (xvalid[p]) {
       Xyzz<F> q = ld_xyzz<G>(xpts + (size_t)p * XW);
-      acc = has ? xyzz_add(acc, q) : q;
+      acc = has ? br_add<G>(acc, q) : q;
       has = true;
     }
   }
@@ -1100,11 +1109,12 @@ __device__ __forceinline__ uint32_t insert_bit(uint32_t t, int bit) {
 template <class G, bool BITS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
                                                 const uint32_t* __restrict__ bstart, int lb, int hb, int W, int sr,
-                                                int sc, int sb, uint32_t* __restrict__ out0,
+                                                int sc, int sb, int segt, uint32_t* __restrict__ out0,
                                                 uint32_t* __restrict__ out1) {
   // Rows and columns are cut into sr / sc segments of <= 256 buckets, one wave
   // each (enough waves for 2^19-bucket windows); C[h][seg], D[l][seg].  Bit
-  // sums are cut into sb segments of <= 256 terms; the host adds segments.
+  // sums are cut into sb segments of segt (64..256) terms; the host adds
+  // segments.
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   __shared__ Xyzz<F> sh[4][32];
@@ -1137,7 +1147,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
       src = src0 + (size_t)bucket0 * XW;
     } else {
       const uint32_t wj = job / sb;
-      t0 = (job % sb) * 256u;  // this job's segment of the term range
+      t0 = (job % sb) * (uint32_t)segt;  // this job's segment of the term range
       uint32_t w = wj / (bb + 1), j = wj % (bb + 1);
       if ((int)j < lb) {  // U_j over D[l][*] with bit j of l set
         src = src1 + (((size_t)w << lb) * sc) * XW;
@@ -1162,8 +1172,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
   // tree over the wave.  One curve-addition call site in one uniform loop (a
   // second inlined copy spills G2); barriers only in the block-uniform tree
   // steps.
-  const uint32_t nload = 256 / 64;
-  const uint32_t tend = BITS ? min(cnt, t0 + 256u) : cnt;
+  const uint32_t nload = BITS ? (uint32_t)segt / 64 : 256 / 64;  // block-uniform
+  const uint32_t tend = BITS ? min(cnt, t0 + (uint32_t)segt) : cnt;
   Xyzz<F> v = xyzz_inf<F>();
   for (uint32_t step = 0; step < nload + 6; step++) {
     Xyzz<F> q;
@@ -1187,7 +1197,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
         act = !xyzz_is_inf(q);
       }
     }
-    if (act) v = xyzz_is_inf(v) ? q : xyzz_add(v, q);
+    if (act) v = xyzz_is_inf(v) ? q : br_add<G>(v, q);
     if (step >= nload) __syncthreads();
   }
   if (live && lane == 0) {
@@ -1263,10 +1273,132 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
         act = !xyzz_is_inf(q);
       }
     }
-    if (act) v = xyzz_is_inf(v) ? q : xyzz_add(v, q);
+    if (act) v = xyzz_is_inf(v) ? q : br_add<G>(v, q);
     if (step >= Lmax) __syncthreads();
   }
   if (live && lane == 0) st_xyzz<G>(dst, v);
+}
+
+// Row / column sums in two kernels that keep every issued addition useful
+// (replaces k_msm_br_strip for windows of >= 2^18 buckets):
+//   k_br_fold:  one lane per strip of S buckets of a row or a column, folded
+//               sequentially with the next bucket's load in flight; no tree,
+//               so no lane idles.  Partials: rows (w, h, s) at
+//               ((w << hb) + h) * (2^lb / S) + s, columns (w, s, l) at
+//               nrow + ((w * (2^hb / S) + s) << lb) + l (adjacent lanes read
+//               adjacent columns).
+//   k_br_lines: one workgroup per 256 partials (one line, or 256 / len
+//               lines), a pairwise tree through LDS whose additions are
+//               packed into the lowest lanes at every level, so a level of
+//               k additions costs ceil(k / 64) wave-additions instead of one
+//               per line (k_msm_br_strip's 6-level in-wave tree issued 6
+//               wave-additions per line for 63 useful lane-additions).
+// Outputs C[w][h] and D[w][l] with one segment per line (sr = sc = 1).
+template <class G, int S>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE)))
+    k_br_fold(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ bstart, int lb, int hb, int W,
+              uint32_t* __restrict__ part) {
+  using F = typename G::F;
+  constexpr int XW = 4 * G::CW;
+  const int bb = lb + hb;
+  const uint32_t per_w = (1u << bb) / S;  // strips per window, per direction
+  const uint32_t nrow = (uint32_t)W * per_w;
+  const uint32_t task = blockIdx.x * 256 + threadIdx.x;
+  if (task >= 2 * nrow) return;
+  uint32_t b0, stride;
+  if (task < nrow) {
+    const uint32_t w = task / per_w, r = task % per_w;
+    const uint32_t h = r / ((1u << lb) / S), s = r % ((1u << lb) / S);
+    b0 = (w << bb) + (h << lb) + s * S;
+    stride = 1;
+  } else {
+    const uint32_t c = task - nrow, w = c / per_w, r = c % per_w;
+    const uint32_t s = r >> lb, l = r & ((1u << lb) - 1);
+    b0 = (w << bb) + ((s * S) << lb) + l;
+    stride = 1u << lb;
+  }
+  Xyzz<F> v = xyzz_inf<F>();
+  Xyzz<F> q = bstart[b0 + 1] > bstart[b0] ? ld_xyzz<G>(buckets + (size_t)b0 * XW) : xyzz_inf<F>();
+  for (int k = 0; k < S; k++) {
+    Xyzz<F> qn = xyzz_inf<F>();
+    if (k + 1 < S) {
+      const uint32_t b = b0 + (uint32_t)(k + 1) * stride;
+      if (bstart[b + 1] > bstart[b]) qn = ld_xyzz<G>(buckets + (size_t)b * XW);
+    }
+    v = br_add<G>(v, q);
+    q = qn;
+  }
+  st_xyzz<G>(part + (size_t)task * XW, v);
+}
+
+template <class G>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE)))
+    k_br_lines(const uint32_t* __restrict__ part, int lb, int hb, int W, int S, uint32_t nwg_rows,
+               uint32_t* __restrict__ outC, uint32_t* __restrict__ outD) {
+  using F = typename G::F;
+  constexpr int XW = 4 * G::CW;
+  extern __shared__ uint32_t sh[];  // 256 packed XYZZ
+  const int bb = lb + hb;
+  const bool rows = blockIdx.x < nwg_rows;
+  const uint32_t len = rows ? (1u << lb) / S : (1u << hb) / S;  // partials per line
+  const uint32_t lenp = len < 256 ? len : 256;                  // per line in the tree
+  const uint32_t m = 256 / lenp;                                // lines per workgroup
+  const uint32_t f = len / lenp;                                // partials folded per lane
+  const uint32_t g = rows ? blockIdx.x : blockIdx.x - nwg_rows;
+  const uint32_t t = threadIdx.x;
+  // load: rows read contiguous partials; columns put adjacent lines on
+  // adjacent lanes (adjacent addresses)
+  uint32_t i, p;
+  if (rows) {
+    i = t / lenp;
+    p = t % lenp;
+  } else {
+    i = t % m;
+    p = t / m;
+  }
+  const uint32_t line = g * m + i;  // (w << hb) + h, or (w << lb) + l
+  uint32_t levels = 0;
+  while ((1u << levels) < lenp) levels++;
+  // one curve-addition call site: f fold steps, then the tree levels
+  Xyzz<F> v = xyzz_inf<F>();
+  for (uint32_t step = 0; step < f + levels; step++) {
+    Xyzz<F> a, b;
+    bool act = true;
+    uint32_t* dst = nullptr;
+    if (step < f) {
+      const uint32_t s = step * lenp + p;
+      size_t idx;
+      if (rows) {
+        idx = (size_t)line * len + s;
+      } else {
+        const uint32_t w = line >> lb, l = line & ((1u << lb) - 1);
+        idx = ((size_t)W << bb) / S + (((size_t)w * len + s) << lb) + l;
+      }
+      a = v;
+      b = ld_xyzz<G>(part + idx * XW);
+    } else {
+      const uint32_t half = lenp >> (step - f + 1);
+      act = t < m * half;
+      if (act) {
+        dst = sh + (size_t)((t / half) * lenp + t % half) * XW;
+        a = ld_xyzz<G>(dst);
+        b = ld_xyzz<G>(dst + (size_t)half * XW);
+      }
+    }
+    if (act) {
+      const Xyzz<F> r = br_add<G>(a, b);
+      if (step < f) v = r;
+      else st_xyzz<G>(dst, r);
+    }
+    if (step + 1 == f) st_xyzz<G>(sh + (size_t)(i * lenp + p) * XW, v);
+    if (step + 1 >= f) __syncthreads();
+  }
+  if (t < m) {
+    const uint32_t ln = g * m + t;
+    const uint32_t* src = sh + (size_t)(t * lenp) * XW;
+    uint32_t* dst = (rows ? outC : outD) + (size_t)ln * XW;
+    for (int k = 0; k < XW; k++) dst[k] = src[k];
+  }
 }
 
 // ------------------------------------------------------------ base upload
@@ -1865,6 +1997,18 @@ static void scan_excl(hipStream_t st, uint32_t* a, size_t len, uint32_t* bsums, 
   k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
 }
 
+// Timing ablation for development only (tools/ablate_msm.py): ZKMI_DEBUG_SKIP
+// bit 1 re-uses a lane's previous sort and item plan (valid only when every
+// MSM on the lane has the same scalars), bit 4 skips the bucket reduction
+// (results wrong).  Never set in tests or the bench.
+static int debug_skip() {
+  static const int v = [] {
+    const char* e = getenv("ZKMI_DEBUG_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // Digits + bucket sort on the lane stream: sval (sorted entries) and bstart
 // (K + 1 bucket starts) in the lane workspace.  The context stream waits only
 // for the digits pass, the one reader of the scalars.
@@ -1910,6 +2054,12 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   ZK_TRY(ws.get("msm_tot", 64, (void**)&tot));
   ZK_HIP(hipEventRecord(lane->fork, ctx->stream));
   ZK_HIP(hipStreamWaitEvent(st, lane->fork, 0));
+  if ((debug_skip() & 1) && lane->debug_sorted) {
+    *out_sval = sval;
+    *out_bstart = bstart;
+    return 0;
+  }
+  lane->debug_sorted = 1;
   ScopedKernelTimer tm(ctx, "msm_sort", st);
   if (!fused) {
     ZK_TRY(dispatch_digits(P.c, st, d_scalars, n, P.p, P.W, digits));
@@ -1963,42 +2113,77 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   return 0;
 }
 
-// Bucket-reduction geometry of a plan.  Windows with rows / columns of >= 2^9
-// buckets: strip-folding waves of contiguous buckets (G1: 8 per lane, 2^20
-// table MSM 0.34 -> 0.28 ms isolated; G2: 16); otherwise <= 256-bucket strided
-// wave jobs.  sb = segments per bit sum (the longest bit job sums
-// max(2^hb * sr, 2^(lb-1) * sc) terms, cut into 256-term segments).
+// Bucket-reduction geometry of a plan.
+//   mode 1 (windows with rows / columns of >= 2^9 buckets, i.e. the >= 2^18
+//     bucket tables): k_msm_br_strip waves of 8 (G1) / 16 (G2) buckets per
+//     lane and a 6-level in-wave tree.
+//   mode 2 (ZKMI_BR_MODE=2, same windows): k_br_fold (S buckets per lane) +
+//     k_br_lines, one C / D segment per line (sr = sc = 1).  Issues ~35% fewer
+//     wave-additions and is 15% faster isolated (2^20 table: 0.38 vs 0.45 ms),
+//     but in the pipelined bench it was level for the 2^20 MSM (755-765 both)
+//     and lost 2-7% in the proofs (L2 27.7 -> 27.0/s, zelana_batch end to end
+//     47.7 -> 44.4/s), so it stays opt-in.  Every level of either form runs
+//     at 1-2 waves per SIMD, where one full XYZZ addition takes ~15-20 us (vs
+//     ~5.5 us of issue at 4+ waves): the ~19 dependent additions from 2^19
+//     buckets to the bit sums set the isolated time.
+//   mode 0 (smaller windows): <= 256-bucket strided wave jobs (k_msm_br).
+// Bit sums: sb segments of segt terms each (the longest bit job sums
+// max(2^hb * sr, 2^(lb-1) * sc) terms); the host adds the segments.  Shorter
+// segments cut the bit kernel's chain of dependent additions (it runs 20-40
+// waves on an otherwise idle chip) for a few more host additions.
 struct BrGeom {
-  bool strip;
-  int sr, sc, sb;
+  int mode;
+  int S;  // mode 2: buckets per lane in k_br_fold
+  int sr, sc, sb, segt;
 };
 static BrGeom br_geom(const MsmPlan& P, bool g2) {
-  static const int strip_fold = [] {  // buckets folded per lane before the tree
+  static const int env_mode = [] {
+    const char* e = getenv("ZKMI_BR_MODE");
+    return e ? atoi(e) : 1;
+  }();
+  static const int strip_fold = [] {  // mode 1: buckets folded per lane before the tree
     const char* e = getenv("ZKMI_BR_STRIP");
     return e ? atoi(e) : 8;
   }();
-  static const int strip_fold2 = [] {  // G2: 16 per lane (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
+  static const int strip_fold2 = [] {  // mode 1, G2 (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
     const char* e = getenv("ZKMI_BR_STRIP_G2");
     return e ? atoi(e) : 16;
   }();
-  const int fold = g2 ? strip_fold2 : strip_fold;
+  // mode 2 defaults, 2^20 table MSM with 3 lanes (tools/br_ab2.sh, interleaved
+  // repeats in tools/perf_table.py): mode 1 1.374 ms/MSM, S = 8 / 128-term
+  // segments 1.312 ms, S = 4 1.342 ms (not reproduced by bench.py, above).
+  static const int env_fold = [] {  // mode 2: buckets per lane (4 or 8)
+    const char* e = getenv("ZKMI_BR_FOLD");
+    return e ? atoi(e) : 0;
+  }();
+  static const int env_seg = [] {  // mode 2: terms per bit-sum segment (64, 128, 256)
+    const char* e = getenv("ZKMI_BR_SEG");
+    return e ? atoi(e) : 0;
+  }();
   BrGeom g;
-  g.strip = fold > 0 && P.hb >= 9;
-  const int segb = g.strip ? 64 * fold : 256;  // buckets per wave job
-  g.sr = (1 << P.lb) > segb ? (1 << P.lb) / segb : 1;
-  g.sc = (1 << P.hb) > segb ? (1 << P.hb) / segb : 1;
+  g.mode = P.hb >= 9 ? (env_mode == 2 ? 2 : 1) : 0;
+  g.S = env_fold == 4 ? 4 : 8;
+  g.segt = 256;
+  if (g.mode == 2) {
+    g.sr = g.sc = 1;
+    g.segt = env_seg == 64 || env_seg == 256 ? env_seg : 128;
+  } else {
+    const int fold = g2 ? strip_fold2 : strip_fold;
+    const int segb = g.mode == 1 ? 64 * fold : 256;  // buckets per wave job
+    g.sr = (1 << P.lb) > segb ? (1 << P.lb) / segb : 1;
+    g.sc = (1 << P.hb) > segb ? (1 << P.hb) / segb : 1;
+  }
   const uint32_t maxterms = std::max((1u << P.hb) * g.sr, (1u << (P.lb - 1)) * g.sc);
-  g.sb = (int)((maxterms + 255) / 256);
+  g.sb = (int)((maxterms + g.segt - 1) / g.segt);
   return g;
 }
 
 // Queue the hand-over of a job's bit sums (W*(bb+1)*sb XYZZ terms, `words`
-// u32 at d_sums) on the lane stream: for a sharded MSM over RCCL, first the
+// u32 at d_sums) on stream st (the lane stream): for a sharded MSM over RCCL, first the
 // all-gather of every rank's bit sums (comm stream, ordered after the lane's
 // work), then the D2H into the job's pinned buffer and the job's event.
-static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, zkmi_msm_job* job, const uint32_t* d_sums,
+static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, hipStream_t st, zkmi_msm_job* job, const uint32_t* d_sums,
                               size_t words) {
-  hipStream_t st = lane->st;
   const int nr = job->comm ? job->comm->nranks : 1;
   const bool dev_gather = job->comm && job->comm->kind == ZKMI_COMM_RCCL;
   const uint32_t* src = d_sums;
@@ -2062,11 +2247,12 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     ZK_TRY(ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
     ZK_TRY(ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
     ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
-    {
+    ZK_HIP(hipMemsetAsync(xkey, 0xFF, xl * 4, st));
+    ZK_HIP(hipMemsetAsync(xvalid, 0, xl * 4, st));
+    if (!((debug_skip() & 1) && lane->debug_sorted == 2)) {
+      lane->debug_sorted = 2;
       ScopedKernelTimer tm(ctx, "msm_items_plan", st);
       ZK_HIP(hipMemsetAsync(hist, 0, (ITEM_CAP_MAX + 1) * 4, st));
-      ZK_HIP(hipMemsetAsync(xkey, 0xFF, xl * 4, st));
-      ZK_HIP(hipMemsetAsync(xvalid, 0, xl * 4, st));
       k_items_count<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hist, hv, &flags[0]);
       scan_excl(st, hv, K, bsums, &nitems[1]);
       k_items_offsets<<<1, 1, 0, st>>>(hist, cap, cursor, &nitems[0]);
@@ -2132,29 +2318,43 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     }
     ZK_HIP(hipGetLastError());
   }
-  // bucket reduction -> W*(bb+1) canonical bit sums
+  // bucket reduction -> W*(bb+1) canonical bit sums.  (Tried: the reduction
+  // and hand-over on a second stream with double-buffered buckets, so the
+  // lane goes on to the next sort: 1.31 -> 1.57 ms per 2^20 MSM with a br
+  // stream per lane -- more streams than the box's 4 hardware queues -- and
+  // 1.37 ms with one shared br stream.)
+  hipStream_t brs = st;
   uint32_t *Cb, *Db, *sums;
   const BrGeom bg = br_geom(P, G::CW != 8);
-  const bool strip = bg.strip;
   const int sr = bg.sr, sc = bg.sc, sb = bg.sb;
   ZK_TRY(ws.get("msm_C", (size_t)W * (1u << hb) * sr * XW * 4, (void**)&Cb));
   ZK_TRY(ws.get("msm_D", (size_t)W * (1u << lb) * sc * XW * 4, (void**)&Db));
   ZK_TRY(ws.get("msm_sums", (size_t)W * (bb + 1) * sb * XW * 4, (void**)&sums));
-  {
-    ScopedKernelTimer tm(ctx, "msm_bucket_reduce", st);
+  if (!(debug_skip() & 4)) {
+    ScopedKernelTimer tm(ctx, "msm_bucket_reduce", brs);
     uint32_t jobs2 = (uint32_t)W * (bb + 1) * sb;
-    if (strip) {  // one wave per row / column
+    if (bg.mode == 2) {
+      const uint32_t nstrips = (uint32_t)W * ((1u << bb) / bg.S);  // per direction
+      uint32_t* part;
+      ZK_TRY(ws.get("msm_brpart", (size_t)2 * nstrips * XW * 4, (void**)&part));
+      const unsigned g1 = (2 * nstrips + 255) / 256;
+      if (bg.S == 8) k_br_fold<G, 8><<<g1, 256, 0, brs>>>(buckets, bstart, lb, hb, W, part);
+      else k_br_fold<G, 4><<<g1, 256, 0, brs>>>(buckets, bstart, lb, hb, W, part);
+      auto wgs = [](uint32_t lines, uint32_t len) { return len >= 256 ? lines : lines / (256 / len); };
+      const uint32_t nwr = wgs((uint32_t)W << hb, (1u << lb) / bg.S), nwc = wgs((uint32_t)W << lb, (1u << hb) / bg.S);
+      k_br_lines<G><<<nwr + nwc, 256, 256 * XW * 4, brs>>>(part, lb, hb, W, bg.S, nwr, Cb, Db);
+    } else if (bg.mode == 1) {  // one wave per row / column
       uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc));
-      k_msm_br_strip<G><<<(jobs1 + 3) / 4, 256, 0, st>>>(buckets, bstart, lb, hb, W, sr, sc, Cb, Db);
+      k_msm_br_strip<G><<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, bstart, lb, hb, W, sr, sc, Cb, Db);
     } else {
       uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc));
-      k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, st>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, Cb, Db);
+      k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, 256, Cb, Db);
     }
-    k_msm_br<G, true><<<(jobs2 + 3) / 4, 256, 0, st>>>(Cb, Db, nullptr, lb, hb, W, sr, sc, sb, sums, nullptr);
+    k_msm_br<G, true><<<(jobs2 + 3) / 4, 256, 0, brs>>>(Cb, Db, nullptr, lb, hb, W, sr, sc, sb, bg.segt, sums, nullptr);
     ZK_HIP(hipGetLastError());
   }
   job->sb = sb;
-  return msm_queue_handover(ctx, lane, job, sums, (size_t)W * (bb + 1) * sb * XW);
+  return msm_queue_handover(ctx, lane, brs, job, sums, (size_t)W * (bb + 1) * sb * XW);
 }
 
 static int msm_acc_any(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const zkmi_bases* tb, size_t offset, size_t n,
@@ -2392,7 +2592,7 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
         set_error("msm_sharded: hipMemsetAsync failed");
         rc = ZKMI_EHIP;
       } else {
-        rc = msm_queue_handover(ctx, lane, job, zeros, words);
+        rc = msm_queue_handover(ctx, lane, lane->st, job, zeros, words);
       }
     }
   }

@@ -44,6 +44,7 @@ struct MsmLane {
   hipStream_t st = nullptr;
   Workspace ws;
   hipEvent_t fork = nullptr, consumed = nullptr;
+  int debug_sorted = 0;  // ZKMI_DEBUG_SKIP ablations only (msm.hip)
 };
 
 struct KernelTimer {
