@@ -17,7 +17,7 @@ n = 1 << log_n
 ctx = Context(0)
 d = ctx.scalars_generate(seed=20, n=n)
 ref = None
-K = 30
+K = int(os.environ.get("K", "30"))
 for cfg, nl in [(c, nl) for c in cfgs for nl in lanes]:
     ctx.set_lanes(nl)
     b = ctx.bases_generate(seed=1000, n=n, g2=g2)

@@ -233,9 +233,10 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_count(const int32_t* __res
 // works (each bin's entries only need to be contiguous in the LDS tile), and
 // this one keeps the LDS accesses conflict-free.  Wave scans by shuffles, one
 // barrier to combine the 4 waves.  tmp has RS_THREADS / 64 words.
+template <int T = RS_THREADS>
 __device__ __forceinline__ uint32_t rs_block_scan(const uint32_t* hist, uint32_t* lstart, uint32_t nb, uint32_t* tmp) {
   uint32_t sum = 0;
-  for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) sum += hist[x];
+  for (uint32_t x = threadIdx.x; x < nb; x += T) sum += hist[x];
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t inc = sum;
 #pragma unroll
@@ -247,12 +248,12 @@ __device__ __forceinline__ uint32_t rs_block_scan(const uint32_t* hist, uint32_t
   __syncthreads();
   uint32_t run = inc - sum, total = 0;
 #pragma unroll
-  for (int w = 0; w < RS_THREADS / 64; w++) {
+  for (int w = 0; w < T / 64; w++) {
     const uint32_t tw = tmp[w];
     if ((uint32_t)w < wid) run += tw;
     total += tw;
   }
-  for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) {
+  for (uint32_t x = threadIdx.x; x < nb; x += T) {
     lstart[x] = run;
     run += hist[x];
   }
@@ -266,16 +267,16 @@ __device__ __forceinline__ uint32_t rs_block_scan(const uint32_t* hist, uint32_t
 // written lines get evicted (measured: ~10x slower than the reads).
 // LDS layout: hist[nb] | lstart[nb] | gbase[nb] | tmp[4] | skey[RS_ST] | sval[RS_ST]
 // Four barriers per sub-tile; hist is zeroed by the caller's first barrier.
-template <int PER, class Fill, class Bin, bool WRITE_KEY>
+template <int PER, class Fill, class Bin, bool WRITE_KEY, int T = RS_THREADS>
 __device__ __forceinline__ void rs_scatter_core(uint32_t nsub, uint32_t nb, uint32_t* lds, Fill fill, Bin bin,
                                                  uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
   uint32_t* hist = lds;
   uint32_t* lstart = lds + nb;
   uint32_t* gbase = lds + 2 * nb;
   uint32_t* tmp = lds + 3 * nb;
-  uint32_t* skey = tmp + RS_THREADS;
-  uint32_t* sval = skey + PER * RS_THREADS;
-  for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) hist[x] = 0;
+  uint32_t* skey = tmp + T;
+  uint32_t* sval = skey + PER * T;
+  for (uint32_t x = threadIdx.x; x < nb; x += T) hist[x] = 0;
   __syncthreads();
   for (uint32_t sub = 0; sub < nsub; sub++) {
     uint32_t key[PER], val[PER], rk[PER];
@@ -285,7 +286,7 @@ __device__ __forceinline__ void rs_scatter_core(uint32_t nsub, uint32_t nb, uint
     for (int k = 0; k < PER; k++)
       if (ok[k]) rk[k] = atomicAdd(&hist[bin(key[k])], 1u);
     __syncthreads();
-    const uint32_t total = rs_block_scan(hist, lstart, nb, tmp);
+    const uint32_t total = rs_block_scan<T>(hist, lstart, nb, tmp);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PER; k++) {
@@ -296,14 +297,14 @@ __device__ __forceinline__ void rs_scatter_core(uint32_t nsub, uint32_t nb, uint
       }
     }
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < total; q += RS_THREADS) {
+    for (uint32_t q = threadIdx.x; q < total; q += T) {
       uint32_t kk = skey[q], bn = bin(kk);
       uint32_t g = gbase[bn] + (q - lstart[bn]);
       if (WRITE_KEY) okey[g] = kk;
       oval[g] = sval[q];
     }
     __syncthreads();
-    for (uint32_t x = threadIdx.x; x < nb; x += RS_THREADS) {
+    for (uint32_t x = threadIdx.x; x < nb; x += T) {
       gbase[x] += hist[x];
       hist[x] = 0;
     }
@@ -312,22 +313,24 @@ __device__ __forceinline__ void rs_scatter_core(uint32_t nsub, uint32_t nb, uint
 }
 
 // entries e in [0, count) from load(e, key, val), RS_ST per sub-tile
-template <int RS_ST, class Load, class Bin, bool WRITE_KEY>
+template <int RS_ST, class Load, class Bin, bool WRITE_KEY, int T = RS_THREADS>
 __device__ __forceinline__ void rs_scatter_tiles(uint32_t count, uint32_t nb, uint32_t* lds, Load load, Bin bin,
                                                  uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
-  constexpr int PER = RS_ST / RS_THREADS;
+  constexpr int PER = RS_ST / T;
   auto fill = [&](uint32_t sub, uint32_t* key, uint32_t* val, bool* ok) {
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-      const uint32_t e = sub * RS_ST + k * RS_THREADS + threadIdx.x;
+      const uint32_t e = sub * RS_ST + k * T + threadIdx.x;
       ok[k] = e < count && load(e, key[k], val[k]);
     }
   };
-  rs_scatter_core<PER, decltype(fill), Bin, WRITE_KEY>((count + RS_ST - 1) / RS_ST, nb, lds, fill, bin, okey, oval);
+  rs_scatter_core<PER, decltype(fill), Bin, WRITE_KEY, T>((count + RS_ST - 1) / RS_ST, nb, lds, fill, bin, okey, oval);
 }
 
 // entries per LDS sub-tile: 4096 or 8192 (longer runs per bin, fewer resident workgroups)
-__host__ __device__ constexpr size_t rs_scatter_lds(uint32_t nb, uint32_t st) { return (3 * (size_t)nb + RS_THREADS + 2 * st) * 4; }
+__host__ __device__ constexpr size_t rs_scatter_lds(uint32_t nb, uint32_t st, uint32_t t = RS_THREADS) {
+  return (3 * (size_t)nb + t + 2 * st) * 4;
+}
 
 template <int RS_ST>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_scatter(const int32_t* __restrict__ digits, uint64_t M,
@@ -389,18 +392,20 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_count(const uint32_t* __r
   for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) cnt1[(size_t)x * nc1 + blockIdx.x] = hist[x];
 }
 
-template <int C>
-__global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_scatter(const uint32_t* __restrict__ scalars, size_t n, int Wp,
+// T threads: a sub-tile is T scalars (T * W entries); 1024 gives 4x longer
+// runs per bin than 256 (one workgroup per CU, 16 waves)
+template <int C, int T>
+__global__ void __launch_bounds__(T) k_rs_p1f_scatter(const uint32_t* __restrict__ scalars, size_t n, int Wp,
                                                                uint32_t B, uint32_t NH, uint32_t lob, uint32_t CS,
                                                                uint32_t nc1, const uint32_t* __restrict__ offs1,
                                                                uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
   extern __shared__ uint32_t lds[];
   constexpr int W = msm_windows(C);
-  for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) lds[2 * NH + x] = offs1[(size_t)x * nc1 + blockIdx.x];
+  for (uint32_t x = threadIdx.x; x < NH; x += T) lds[2 * NH + x] = offs1[(size_t)x * nc1 + blockIdx.x];
   const size_t base = (size_t)blockIdx.x * CS;
   const uint32_t cnt = (uint32_t)std::min<size_t>(CS, n - base);
   auto fill = [&](uint32_t sub, uint32_t* key, uint32_t* val, bool* ok) {
-    const uint32_t k = sub * RS_THREADS + threadIdx.x;
+    const uint32_t k = sub * T + threadIdx.x;
     if (k < cnt) {
       rs_scalar_keys<C>(scalars, base + k, n, Wp, B, key, val, ok);
     } else {
@@ -409,7 +414,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_scatter(const uint32_t* _
     }
   };
   auto bin = [lob](uint32_t key) { return key >> lob; };
-  rs_scatter_core<W, decltype(fill), decltype(bin), true>((cnt + RS_THREADS - 1) / RS_THREADS, NH, lds, fill, bin,
+  rs_scatter_core<W, decltype(fill), decltype(bin), true, T>((cnt + T - 1) / T, NH, lds, fill, bin,
                                                           okey, oval);
 }
 
@@ -496,8 +501,8 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p2_count(const uint32_t* __re
     cnt2[((size_t)tstart[h] << lob) + (size_t)x * nt + q] = hist[x];
 }
 
-template <int RS_ST>
-__global__ void __launch_bounds__(RS_THREADS) k_rs_p2_scatter(const uint32_t* __restrict__ okey,
+template <int RS_ST, int T = RS_THREADS>
+__global__ void __launch_bounds__(T) k_rs_p2_scatter(const uint32_t* __restrict__ okey,
                                                               const uint32_t* __restrict__ oval,
                                                               const uint32_t* __restrict__ binstart,
                                                               const uint32_t* __restrict__ tstart, uint32_t NH,
@@ -510,7 +515,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p2_scatter(const uint32_t* __
   if (t >= tstart[NH]) return;
   const uint32_t h = rs_tile_bin(tstart, NH, t), q = t - tstart[h], nt = tstart[h + 1] - tstart[h];
   const uint32_t lo = binstart[h] + q * C2, hi = min(lo + C2, binstart[h + 1]);
-  for (uint32_t x = threadIdx.x; x < NLO; x += RS_THREADS)
+  for (uint32_t x = threadIdx.x; x < NLO; x += T)
     lds[2 * NLO + x] = offs2[((size_t)tstart[h] << lob) + (size_t)x * nt + q];
   auto load = [&](uint32_t e, uint32_t& key, uint32_t& val) {
     key = okey[lo + e];
@@ -518,7 +523,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p2_scatter(const uint32_t* __
     return true;
   };
   auto bin = [mask](uint32_t key) { return key & mask; };
-  rs_scatter_tiles<RS_ST, decltype(load), decltype(bin), false>(hi - lo, NLO, lds, load, bin, nullptr, sval);
+  rs_scatter_tiles<RS_ST, decltype(load), decltype(bin), false, T>(hi - lo, NLO, lds, load, bin, nullptr, sval);
 }
 
 // bucket starts: start of key k = scanned count at (hi, lo, tile 0)
@@ -1906,8 +1911,19 @@ template <int C>
 static void launch_p1_fused(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t NH,
                             uint32_t lob, uint32_t CS, uint32_t nf, uint32_t* cnt1, uint32_t* okey, uint32_t* oval,
                             bool scatter) {
-  if (scatter)
-    k_rs_p1f_scatter<C><<<nf, RS_THREADS, rs_scatter_lds(NH, RS_THREADS * msm_windows(C)), st>>>(
+  // sub-tiles of 1024 scalars when their LDS fits (c >= 15: W <= 17), else
+  // 256: 2^26 table MSM sort 12.2 -> 10.4 ms isolated (P1 runs 6 -> 24
+  // entries per bin; tools/rs_ab.sh)
+  static const int env_t1 = [] {
+    const char* e = getenv("ZKMI_RS_T1");
+    return e ? atoi(e) : 1024;
+  }();
+  constexpr int W = msm_windows(C);
+  if (scatter && env_t1 == 1024 && rs_scatter_lds(NH, 1024 * W, 1024) <= 160 * 1024)
+    k_rs_p1f_scatter<C, 1024><<<nf, 1024, rs_scatter_lds(NH, 1024 * W, 1024), st>>>(sc, n, Wp, B, NH, lob, CS, nf,
+                                                                                    cnt1, okey, oval);
+  else if (scatter)
+    k_rs_p1f_scatter<C, RS_THREADS><<<nf, RS_THREADS, rs_scatter_lds(NH, RS_THREADS * W), st>>>(
         sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval);
   else
     k_rs_p1f_count<C><<<nf, RS_THREADS, NH * 4, st>>>(sc, n, Wp, B, NH, lob, CS, nf, cnt1);
@@ -2074,9 +2090,9 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   };
   static const int env_st1 = [] { const char* e = getenv("ZKMI_RS_ST1"); return e ? atoi(e) : 4096; }();
   static const int env_st2 = [] { const char* e = getenv("ZKMI_RS_ST2"); return e ? atoi(e) : 0; }();
-  // P2 sub-tiles of 8192 entries (runs twice as long per lo bin) pay off for
-  // large sorts (2^26 table MSM: P2 scatter -1 ms) and lose on small ones
-  const int st2 = env_st2 ? env_st2 : (Mmax >= (size_t(1) << 26) ? 8192 : 4096);
+  // P2 sub-tiles of 8192 entries (runs twice as long per lo bin; with 256
+  // threads they paid off only for >= 2^26 entries, with 1024 for all sizes)
+  const int st2 = env_st2 ? env_st2 : 8192;
   const uint32_t ne = (uint32_t)P.ne;
   if (fused) {
     ZK_TRY(p1_fused(P.c, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, nullptr, nullptr, false));
@@ -2101,12 +2117,19 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   k_rs_p2_count<<<g2, RS_THREADS, (1u << lob) * 4, st>>>(okey, binstart, tstart, NH, lob, C2, T2max, cnt2);
   scan(cnt2, len2, &tot[1]);
   k_rs_bstart<<<(P.K + 256) / 256, 256, 0, st>>>(cnt2, binstart, tstart, NH, lob, P.K, bstart);
-  if (st2 == 8192 && rs_scatter_lds(1u << lob, 8192) <= 160 * 1024)
-    k_rs_p2_scatter<8192><<<g2, RS_THREADS, rs_scatter_lds(1u << lob, 8192), st>>>(okey, oval, binstart, tstart, NH, lob, C2, T2max,
-                                                                     cnt2, sval);
-  else
-    k_rs_p2_scatter<4096><<<g2, RS_THREADS, rs_scatter_lds(1u << lob, 4096), st>>>(okey, oval, binstart, tstart, NH, lob, C2, T2max,
-                                                                     cnt2, sval);
+  // 1024-thread P2 workgroups over 8192-entry sub-tiles (2^20 table MSM, 3
+  // lanes, interleaved repeats: 1.344 -> 1.297 ms with the 1024-thread P1;
+  // tools/rs_ab2.sh)
+  static const int env_t2 = [] { const char* e = getenv("ZKMI_RS_T2"); return e ? atoi(e) : 1024; }();
+  const uint32_t NLO = 1u << lob;
+#define ZK_P2(ST, T) \
+  k_rs_p2_scatter<ST, T><<<g2, T, rs_scatter_lds(NLO, ST, T), st>>>(okey, oval, binstart, tstart, NH, lob, C2, T2max, cnt2, sval)
+  if (env_t2 == 1024 && st2 == 16384 && rs_scatter_lds(NLO, 16384, 1024) <= 160 * 1024) ZK_P2(16384, 1024);
+  else if (env_t2 == 1024 && st2 >= 8192 && rs_scatter_lds(NLO, 8192, 1024) <= 160 * 1024) ZK_P2(8192, 1024);
+  else if (env_t2 == 1024) ZK_P2(4096, 1024);
+  else if (st2 == 8192 && rs_scatter_lds(NLO, 8192) <= 160 * 1024) ZK_P2(8192, RS_THREADS);
+  else ZK_P2(4096, RS_THREADS);
+#undef ZK_P2
   ZK_HIP(hipGetLastError());
   *out_sval = sval;
   *out_bstart = bstart;
