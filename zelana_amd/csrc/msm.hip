@@ -2038,8 +2038,9 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   while ((1u << kb) < P.K) kb++;
   static const int env_lob = [] { const char* e = getenv("ZKMI_RS_LOB"); return e ? atoi(e) : 0; }();
   static const int env_c2 = [] { const char* e = getenv("ZKMI_RS_C2"); return e ? atoi(e) : 0; }();
-  // 21-bit keys (c = 22 tables): 9 hi bits, 12 lo (2^26: 0.8 ms faster than 8 + 13)
-  const uint32_t lob = env_lob ? (uint32_t)env_lob : (kb > 20 ? kb - 9 : kb > 16 ? kb - 8 : 8);
+  // 21-bit keys (c = 22 tables): 10 hi bits, 11 lo (2^26 with the 1024-thread
+  // scatters: sort 10.5 -> 9.4 ms vs 9 + 12, 13.2 ms for 8 + 13; tools/rs_lob.sh)
+  const uint32_t lob = env_lob ? (uint32_t)env_lob : (kb > 20 ? kb - 10 : kb > 16 ? kb - 8 : 8);
   const uint32_t NH = (P.K + (1u << lob) - 1) >> lob;
   const size_t Mmax = P.Mmax;
   // radix-sort geometry (see k_rs_*): ~2K P1 chunks, ~8K P2 tiles at most
