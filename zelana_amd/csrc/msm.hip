@@ -811,6 +811,10 @@ __device__ __forceinline__ void msm_acc0_body(const uint32_t* __restrict__ sval,
 #ifndef ZK_ACC0_G2_MINBLK
 #define ZK_ACC0_G2_MINBLK 2
 #endif
+// (Tried: the G1 base prefetch through global_load_lds into LDS instead of 16
+// VGPRs, 142 -> 128 VGPRs = 4 waves/SIMD instead of 3: accumulation 1% faster
+// isolated, pipelined 2^20 MSM 3% slower; spilling to reach 4-5 waves: +4% /
+// +42%.  PMC: 2.6 resident waves/SIMD on average.)
 #ifndef ZK_ACC0_G1_MINBLK
 #define ZK_ACC0_G1_MINBLK 1
 #endif
