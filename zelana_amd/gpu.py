@@ -123,6 +123,11 @@ class Context:
 
     def set_lanes(self, lanes: int):
         check(lib().zkmi_msm_set_lanes(self.h, lanes))
+        self._lanes = lanes
+
+    def lanes(self) -> int:
+        """MSM lanes last set through set_lanes (the context's default is 2)."""
+        return getattr(self, "_lanes", 2)
 
     def sync(self):
         check(lib().zkmi_sync(self.h))
