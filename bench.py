@@ -589,6 +589,37 @@ def bench_zbatch(ctx, steps, world, sync_all, allmax):
     sync_all()
     e2e_gpu = allmax(e2e_gpu_local)
     gpu_wit_proof_equal = all(np.array_equal(x, y) for x, y in zip(last, proof))
+    # the same with NB batches per witness run (zkmi_wprog_run_many: the
+    # witness kernels are latency-bound, so NB batches cost about one run);
+    # two alternating buffer sets of NB z's
+    NB = 4
+    zstride = (z.nbytes + 255) // 256 * 256
+    zsets = [gpu.DeviceBuffer(ctx, NB * zstride) for _ in range(2)]
+    zviews = [[zs.view(k * zstride, z.nbytes) for k in range(NB)] for zs in zsets]
+    groups = max(2, (2 * steps + NB - 1) // NB)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        wp.run_many([zbatch.batch_inputs(d) for _ in range(NB)], zsets[0], zstride)
+    ctx.sync()
+    wit_gpu_many = (time.perf_counter() - t0) / (steps * NB)
+    sync_all()
+    t0 = time.perf_counter()
+    inflight = deque()
+    for g in range(groups):
+        wp.run_many([zbatch.batch_inputs(d) for _ in range(NB)], zsets[g % 2], zstride, async_=True)
+        jobs = [gpu.groth16_prove_submit(ctx, pk, dev, zv, r, s) for zv in zviews[g % 2]]
+        while inflight:  # the previous group's proofs (their z set is written by the NEXT run)
+            last_many = gpu.groth16_prove_wait(inflight.popleft())
+        inflight.extend(jobs)
+    while inflight:
+        last_many = gpu.groth16_prove_wait(inflight.popleft())
+    ctx.sync()
+    e2e_many_local = (time.perf_counter() - t0) / (groups * NB)
+    sync_all()
+    e2e_many = allmax(e2e_many_local)
+    many_equal = all(np.array_equal(x, y) for x, y in zip(last_many, proof))
+    del zviews, zsets
     wstats = plan.stats()
     wp.close()
     del dev, pk
@@ -606,6 +637,11 @@ def bench_zbatch(ctx, steps, world, sync_all, allmax):
                        "what": "per batch: Prover.toml inputs -> GPU witness program (z written in HBM, beside the "
                                "previous proof) -> prove",
                        "witness_program": wstats,
+                       "batched": {"batches_per_witness_run": NB, "proofs_per_s": round(world / e2e_many, 3),
+                                   "witness_ms_per_batch_gpu": round(wit_gpu_many * 1e3, 2),
+                                   "ms_per_batch": round(e2e_many * 1e3, 2), "proof_equal": many_equal,
+                                   "what": "the same, NB batches' witnesses in one zkmi_wprog_run_many beside the "
+                                           "previous NB proofs (two alternating sets of NB z buffers)"},
                        "host_witness": {"proofs_per_s": round(world / e2e, 3), "ms_per_batch": round(e2e * 1e3, 2),
                                         "witness_ms_per_batch": round(wit / steps * 1e3, 2), "witness_equal": same_z,
                                         "what": "host builder witness + H2D of z + prove"}},

@@ -320,6 +320,13 @@ void zkmi_wprog_destroy(zkmi_wprog* prog);
  * proof); it then waits only for context work queued before the PREVIOUS
  * run, so callers alternate two z buffers. */
 int zkmi_wprog_run(zkmi_ctx* ctx, zkmi_wprog* prog, const uint64_t* inputs, void* d_z, int async);
+/* nb batches in one run (one launch sequence; the kernels are latency-bound,
+ * so nb batches take about the time of one): inputs = nb x num_inputs x 4
+ * u64, batch i's z at d_z + i * z_stride bytes (z_stride >= num_vars * 32, a
+ * multiple of 32).  Same ordering rules as zkmi_wprog_run, with buffer sets in
+ * place of buffers. */
+int zkmi_wprog_run_many(zkmi_ctx* ctx, zkmi_wprog* prog, size_t nb, const uint64_t* inputs, void* d_z,
+                        size_t z_stride, int async);
 
 /* ------------------------------------------------- verification / on-chain
  * Host code (no GPU needed).  The reference's Groth16Prover::verify is a

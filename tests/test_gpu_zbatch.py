@@ -148,4 +148,30 @@ def test_gpu_witness_program_full(ctx):
     for k, o in outs:
         for g, w in zip(o, want[k]):
             assert np.array_equal(g, w)
+    # several batches per run (zkmi_wprog_run_many): each z equals its host
+    # z; then groups of 3 witnesses beside the previous group's 3 proofs
+    zstride = (z.nbytes + 255) // 256 * 256
+    sets = [gpu.DeviceBuffer(ctx, 3 * zstride) for _ in range(2)]
+    views = [[b.view(i * zstride, z.nbytes) for i in range(3)] for b in sets]
+    group = [(d2, 1), (d, 0), (d2, 1)]
+    wp.run_many([Z.batch_inputs(dd) for dd, _ in group], sets[0], zstride)
+    for (dd, k), v in zip(group, views[0]):
+        got = np.zeros_like(z)
+        v.download(got)
+        assert np.array_equal(got, (z, z2)[k])
+    inflight, outs = deque(), []
+    for gi, grp in enumerate((group, group[::-1], group, group[::-1])):
+        wp.run_many([Z.batch_inputs(dd) for dd, _ in grp], sets[gi % 2], zstride, async_=True)
+        jobs = [(k, gpu.groth16_prove_submit(ctx, pk, dev, v, 11 + k, 13 + k)) for (_, k), v in zip(grp, views[gi % 2])]
+        while inflight:
+            kk, j = inflight.popleft()
+            outs.append((kk, gpu.groth16_prove_wait(j)))
+        inflight.extend(jobs)
+    while inflight:
+        kk, j = inflight.popleft()
+        outs.append((kk, gpu.groth16_prove_wait(j)))
+    assert len(outs) == 12
+    for k, o in outs:
+        for g, w in zip(o, want[k]):
+            assert np.array_equal(g, w)
     wp.close()

@@ -108,6 +108,7 @@ SIGNATURES = [
     ("zkmi_wprog_create", ctypes.c_int, [vp, ctypes.POINTER(WprogDesc), ctypes.POINTER(vp)]),
     ("zkmi_wprog_destroy", None, [vp]),
     ("zkmi_wprog_run", ctypes.c_int, [vp, vp, u64p, vp, ctypes.c_int]),
+    ("zkmi_wprog_run_many", ctypes.c_int, [vp, vp, ctypes.c_size_t, u64p, vp, ctypes.c_size_t, ctypes.c_int]),
     ("zkmi_groth16_verify", ctypes.c_int, [u8p, sz, u64p, sz, u64p, u64p, u64p, ctypes.POINTER(ctypes.c_int)]),
     ("zkmi_alt_bn128_pairing", ctypes.c_int, [u8p, sz, u8p]),
     ("zkmi_alt_bn128_g1_add", ctypes.c_int, [u8p, u8p]),

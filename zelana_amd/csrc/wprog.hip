@@ -237,7 +237,9 @@ __device__ __forceinline__ Fe sel(bool c, const Fe& a, const Fe& b) {
 __global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ ops, uint32_t lo, uint32_t hi,
                                                      const uint2* __restrict__ terms,
                                                      const uint32_t* __restrict__ coeff_m,
-                                                     const uint32_t* __restrict__ rc_m, uint32_t* __restrict__ z) {
+                                                     const uint32_t* __restrict__ rc_m, uint32_t* __restrict__ z,
+                                                     size_t zstride) {
+  z += blockIdx.y * zstride;  // batch blockIdx.y of a multi-batch run
   // Round constants in LDS: a global load inside the round loop would make
   // every round wait (vmcnt) for the previous round's stores to land.
   __shared__ uint32_t rc_s[MIMC_R * 8];
@@ -299,8 +301,9 @@ __global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ o
 // Montgomery -> canonical for the first 4*91 - 1 trace values of every
 // permutation (the last one, its output, is stored canonical)
 __global__ void __launch_bounds__(256) k_wprog_canon(const uint32_t* __restrict__ perm_out, uint32_t nperm,
-                                                     uint32_t* __restrict__ z) {
+                                                     uint32_t* __restrict__ z, size_t zstride) {
   constexpr uint32_t PER = 4 * MIMC_R - 1;
+  z += blockIdx.y * zstride;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nperm * PER) return;
   const uint32_t var = perm_out[i / PER] + i % PER;
@@ -308,8 +311,10 @@ __global__ void __launch_bounds__(256) k_wprog_canon(const uint32_t* __restrict_
 }
 
 __global__ void __launch_bounds__(256) k_wprog_inputs(const uint32_t* __restrict__ in, const uint32_t* __restrict__ var,
-                                                      uint32_t n, uint32_t* __restrict__ z) {
+                                                      uint32_t n, uint32_t* __restrict__ z, size_t zstride) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  z += blockIdx.y * zstride;
+  in += (size_t)blockIdx.y * n * 8;
   if (i >= n) return;
   const uint4* s = reinterpret_cast<const uint4*>(in + (size_t)i * 8);
   uint4* d = reinterpret_cast<uint4*>(z + (size_t)var[i] * 8);
@@ -345,6 +350,7 @@ struct zkmi_wprog {
   uint64_t* h_in[2] = {nullptr, nullptr};  // pinned staging of the inputs (alternating)
   hipEvent_t in_done[2] = {nullptr, nullptr};
   int next_in = 0;
+  size_t in_cap = 1;  // batches h_in / d_in hold
 };
 
 namespace zk {
@@ -488,46 +494,70 @@ void zkmi_wprog_destroy(zkmi_wprog* p) {
   wprog_free(p);
 }
 
-int zkmi_wprog_run(zkmi_ctx* ctx, zkmi_wprog* p, const uint64_t* inputs, void* d_z, int async) {
+int zkmi_wprog_run_many(zkmi_ctx* ctx, zkmi_wprog* p, size_t nb, const uint64_t* inputs, void* d_z,
+                        size_t z_stride, int async) {
   ZK_DEVICE_GUARD(ctx);
-  if (!ctx || !p || !inputs || !d_z || p->ctx != ctx) {
+  if (!ctx || !p || !inputs || !d_z || p->ctx != ctx || nb == 0 || nb > 65535 ||
+      (nb > 1 && (z_stride < p->num_vars * 32 || z_stride % 32))) {
     set_error("zkmi_wprog_run: bad arguments");
     return ZKMI_EINVAL;
   }
   hipStream_t st = p->st;
   // The z this run writes was last read by context work enqueued before the
-  // previous run (callers alternate two z buffers): wait for exactly that,
-  // so this run overlaps the previous batch's proof.  Synchronous runs wait
-  // for the whole context first.
+  // previous run (callers alternate two z buffers / buffer sets): wait for
+  // exactly that, so this run overlaps the previous batches' proofs.
+  // Synchronous runs wait for the whole context first.
   if (!async) ZK_TRY(ctx_sync_all(ctx));
+  const size_t in_bytes = p->num_inputs * 32;
+  if (nb > p->in_cap) {  // grow the input staging (both halves idle after these waits)
+    ZK_HIP(hipEventSynchronize(p->in_done[0]));
+    ZK_HIP(hipEventSynchronize(p->in_done[1]));
+    ZK_HIP(hipStreamSynchronize(st));
+    for (int b = 0; b < 2; b++) {
+      ZK_HIP(hipHostFree(p->h_in[b]));
+      p->h_in[b] = nullptr;
+    }
+    ZK_HIP(hipFree(p->d_in));
+    p->d_in = nullptr;
+    if (hipHostMalloc(&p->h_in[0], nb * in_bytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&p->h_in[1], nb * in_bytes, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&p->d_in, nb * in_bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("zkmi_wprog_run: cannot allocate input staging for %zu batches", nb);
+      return ZKMI_ENOMEM;
+    }
+    p->in_cap = nb;
+  }
   const int b = p->next_in;
   p->next_in ^= 1;
   ZK_HIP(hipEventSynchronize(p->in_done[b]));  // that staging buffer's last upload has landed
-  memcpy(p->h_in[b], inputs, p->num_inputs * 32);
+  memcpy(p->h_in[b], inputs, nb * in_bytes);
   if (p->have_mark) ZK_HIP(hipStreamWaitEvent(st, p->ctx_mark, 0));
   uint32_t* z = (uint32_t*)d_z;
+  const size_t zs = nb > 1 ? z_stride / 4 : 0;  // words
+  const unsigned nby = (unsigned)nb;
   ScopedKernelTimer tm(ctx, "wprog", st);
-  ZK_HIP(hipMemcpyAsync(p->d_in, p->h_in[b], p->num_inputs * 32, hipMemcpyHostToDevice, st));
+  ZK_HIP(hipMemcpyAsync(p->d_in, p->h_in[b], nb * in_bytes, hipMemcpyHostToDevice, st));
   ZK_HIP(hipEventRecord(p->in_done[b], st));
-  k_wprog_inputs<<<(unsigned)((p->num_inputs + 255) / 256), 256, 0, st>>>(p->d_in, p->d_input_var,
-                                                                        (uint32_t)p->num_inputs, z);
+  k_wprog_inputs<<<dim3((unsigned)((p->num_inputs + 255) / 256), nby), 256, 0, st>>>(
+      p->d_in, p->d_input_var, (uint32_t)p->num_inputs, z, zs);
   for (size_t l = 0; l + 1 < p->level_start.size(); l++) {
     const uint32_t lo = p->level_start[l], hi = p->level_start[l + 1];
     if (hi == lo) continue;
     const size_t threads = (size_t)(hi - lo) * 4;
-    k_wprog_level<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(p->d_ops, lo, hi, p->d_terms, p->d_coeff,
-                                                                    p->d_rc, z);
+    k_wprog_level<<<dim3((unsigned)((threads + 255) / 256), nby), 256, 0, st>>>(p->d_ops, lo, hi, p->d_terms,
+                                                                              p->d_coeff, p->d_rc, z, zs);
   }
   if (p->num_perms) {
     const size_t nconv = (size_t)p->num_perms * (4 * MIMC_R - 1);
-    k_wprog_canon<<<(unsigned)((nconv + 255) / 256), 256, 0, st>>>(p->d_perm_out, p->num_perms, z);
+    k_wprog_canon<<<dim3((unsigned)((nconv + 255) / 256), nby), 256, 0, st>>>(p->d_perm_out, p->num_perms, z, zs);
   }
   ZK_HIP(hipGetLastError());
   ZK_HIP(hipEventRecord(p->done, st));
-  // later context work (the proof over this z) waits for the witness
+  // later context work (the proofs over these z) waits for the witness
   ZK_HIP(hipStreamWaitEvent(ctx->stream, p->done, 0));  // MSM lanes fork from the context stream
-  // everything enqueued on the context so far (the previous proof, which
-  // reads the other z buffer) must finish before the NEXT run writes it
+  // everything enqueued on the context so far (the previous proofs, which
+  // read the other z buffers) must finish before the NEXT run writes them
   ZK_HIP(hipEventRecord(p->ctx_mark, ctx->stream));
   p->have_mark = true;
   if (!async) {
@@ -535,6 +565,10 @@ int zkmi_wprog_run(zkmi_ctx* ctx, zkmi_wprog* p, const uint64_t* inputs, void* d
     return timer_flush(ctx);
   }
   return 0;
+}
+
+int zkmi_wprog_run(zkmi_ctx* ctx, zkmi_wprog* p, const uint64_t* inputs, void* d_z, int async) {
+  return zkmi_wprog_run_many(ctx, p, 1, inputs, d_z, 0, async);
 }
 
 }  // extern "C"

@@ -33,6 +33,11 @@ class DeviceBuffer:
         check(lib().zkmi_d2h(self.ctx.h, arr.ctypes.data_as(vp), self.ptr, arr.nbytes), "zkmi_d2h")
         return arr
 
+    def view(self, offset: int, nbytes: int) -> "DeviceView":
+        """[offset, offset + nbytes) of this buffer (no ownership)."""
+        assert 0 <= offset and offset + nbytes <= self.nbytes
+        return DeviceView(self, offset, nbytes)
+
     def free(self):
         if self.ptr:
             lib().zkmi_dev_free(self.ctx.h, self.ptr)
@@ -43,6 +48,18 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+class DeviceView(DeviceBuffer):
+    """A sub-range of a DeviceBuffer (e.g. one batch's z in a multi-batch
+    witness buffer); keeps its parent alive and never frees."""
+
+    def __init__(self, parent: DeviceBuffer, offset: int, nbytes: int):
+        self.ctx, self.nbytes, self.parent = parent.ctx, nbytes, parent
+        self.ptr = vp(parent.ptr.value + offset)
+
+    def free(self):
+        self.ptr = vp()
 
 
 class Bases:

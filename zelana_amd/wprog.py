@@ -187,6 +187,18 @@ class WitnessProgram:
         check(lib().zkmi_wprog_run(self.ctx.h, self.h, inp.ctypes.data_as(u64p), dz.ptr, int(async_)),
               "zkmi_wprog_run")
 
+    def run_many(self, inputs: list, dz, stride: int, async_: bool = False):
+        """len(inputs) batches in one run (zkmi_wprog_run_many): batch i's z at
+        dz + i * stride bytes.  The kernels are latency-bound, so several
+        batches take about the time of one."""
+        inp = np.ascontiguousarray(np.stack([np.asarray(x, np.uint64) for x in inputs]), np.uint64)
+        nb = inp.shape[0]
+        assert inp.shape[1:] == (self.plan.input_var.size, 4), inp.shape
+        assert stride >= self.plan.num_vars * 32 and stride % 32 == 0 and dz.nbytes >= (nb - 1) * stride + \
+            self.plan.num_vars * 32
+        check(lib().zkmi_wprog_run_many(self.ctx.h, self.h, nb, inp.ctypes.data_as(u64p), dz.ptr, stride,
+                                        int(async_)), "zkmi_wprog_run_many")
+
     def close(self):
         if self.h:
             lib().zkmi_wprog_destroy(self.h)
