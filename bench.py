@@ -203,7 +203,7 @@ def main():
     kavg_s = ktot / max(kcnt, 1) / 1e3
     achieved = MSM_BYTES_PER_PAIR * n / kavg_s / 1e9 if kcnt else None
     # acc0_g1 launches before the roofline pass (for tools/rocpd_summary.py)
-    rf_first = ((0 if args.no_plain else 1 + 2 * max(1, args.steps // 2)) + args.warmup
+    rf_first = ((0 if args.no_plain else 2 * args.lanes + 2 * max(1, args.steps // 2)) + args.warmup
                 + args.steps * (1 if args.timers_in_timed_region else 2))
     pairs_total = n * world * args.steps
     value = pairs_total / elapsed / 1e6
