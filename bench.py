@@ -231,11 +231,15 @@ def main():
     if not args.no_zbatch:
         log("zelana_batch proofs")
         extra["zelana_batch_proofs"], zb_state = bench_zbatch(ctx, args.l2_steps, world, sync_all, allmax)
+    c1_state = None
+    if not args.no_l2:
+        log("config 1: L2BlockCircuit proof through Groth16Prover")
+        extra["config1_l2_small"], c1_state = bench_config1(ctx)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baseline legs")
         cpu = cpu_baseline(ctx, bases, scalars, n, result, args.cpu_threads, ntt_state,
-                           None if args.no_cpu_prove else zb_state)
+                           None if args.no_cpu_prove else zb_state, c1_state)
 
     pmc = pmc_record(kernel, args.log_n)
     traffic = pmc.get("hbm_bytes")
@@ -495,6 +499,90 @@ def bench_l2(ctx, log_n, steps, rank, world, sync_all, allmax):
     }
 
 
+def bench_config1(ctx, steps=5):
+    """BASELINE.json configs[0]: the prover crate's own path on one small L2
+    proof -- Groth16Prover.prove(inputs, witness) (prover.rs:350-425) over
+    L2BlockCircuit with the keygen.rs flow (StdRng(0) over dummy(); the GPU
+    key equals arkworks' key byte for byte), timed per call: host synthesis +
+    GPU prove + Solana encoding.  The CPU port proves the same R1CS, z, r, s
+    in the cpu_baseline leg 'config1'."""
+    from zelana_amd.keygen import circuit_specific_setup
+    from zelana_amd.l2block import L2BlockCircuit
+    from zelana_amd.prover import (AccountStateSnapshot, BatchPublicInputs, BatchWitness, Groth16Prover, Transfer,
+                                   l2_block_circuit)
+    from zelana_amd.rng import StdRng
+
+    t0 = time.perf_counter()
+    cs0, _, _ = L2BlockCircuit.dummy().synthesize()
+    pk, vk = circuit_specific_setup(ctx, cs0, StdRng.seed_from_u64(0))
+    pk.precompute()
+    keygen_s = time.perf_counter() - t0
+    prover = Groth16Prover(ctx, pk, vk)
+    sender, recipient = bytes([1] * 32), bytes([2] * 32)
+    w = BatchWitness(transactions=[Transfer(sender, recipient, 100)],
+                     pre_account_states=[AccountStateSnapshot(sender, 1000), AccountStateSnapshot(recipient, 0)])
+    inp = BatchPublicInputs(batch_id=42, batch_hash=bytes(range(32)))
+    prover.prove(inp, w)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        proof = prover.prove(inp, w)
+    dt = (time.perf_counter() - t0) / steps
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        cs, z = l2_block_circuit(inp, w)
+    synth = (time.perf_counter() - t0) / steps
+    # the GPU part alone, on the same R1CS and z: with the CSR and z uploaded
+    # per call (zkmi_groth16_prove), and resident (zkmi_groth16_prove_resident)
+    from zelana_amd import gpu
+    from zelana_amd.prover import _as_z
+    rng = StdRng.seed_from_u64(42)
+    r, s = rng.fr_rand(), rng.fr_rand()
+    zarr = _as_z(z)
+    gpu.groth16_prove(ctx, pk, cs, zarr, r, s)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gpu.groth16_prove(ctx, pk, cs, zarr, r, s)
+    g_up = (time.perf_counter() - t0) / steps
+    dev = gpu.R1CSDevice(ctx, cs)
+    dz = gpu.DeviceBuffer(ctx, zarr.nbytes)
+    dz.upload(zarr)
+    gpu.groth16_prove_resident(ctx, pk, dev, dz, r, s)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = gpu.groth16_prove_resident(ctx, pk, dev, dz, r, s)
+    g_res = (time.perf_counter() - t0) / steps
+    same = all(np.array_equal(x, y) for x, y in zip(res, (proof.a, proof.b, proof.c)))
+    del dev, dz
+    # the native prove() surface: zp::Groth16Prover (C++ host mirror, synthesis
+    # in C++) over libzkmi with the same key bytes
+    from zelana_amd.host_prover import NativeGroth16Prover
+    native = NativeGroth16Prover(pk.serialize(), vk, ctx.device)
+    nbytes, _ = native.prove(inp, w)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        nbytes, _ = native.prove(inp, w)
+    g_nat = (time.perf_counter() - t0) / steps
+    native.close()
+    line = {
+        "workload": f"configs[0]: Groth16Prover.prove over L2BlockCircuit, {cs.num_constraints} constraints "
+                    "(dummy() shape, one transfer, batch_id 42), key from keygen.rs's StdRng(0) flow built on the GPU",
+        "ms_per_proof": round(dt * 1e3, 2), "proofs_per_s": round(1.0 / dt, 2),
+        "host_synthesis_ms": round(synth * 1e3, 2), "keygen_s_gpu": round(keygen_s, 3),
+        "gpu_prove_ms": round(g_up * 1e3, 2), "gpu_prove_resident_ms": round(g_res * 1e3, 2),
+        "resident_proof_equal": same,
+        "native_prove_ms": round(g_nat * 1e3, 2), "native_proof_equal": nbytes == proof.proof_bytes,
+        "note": "native_prove_ms = zp::Groth16Prover::prove (libzelana_prover.so: C++ synthesis + libzkmi), the "
+                "drop-in surface; ms_per_proof = the Python mirror's prove() (its Python R1CS synthesis and CSR "
+                "conversion dominate); gpu_prove_ms = the same R1CS and z through zkmi_groth16_prove (CSR + z uploaded per call), "
+                "gpu_prove_resident_ms = through zkmi_groth16_prove_resident; cpu_baseline.legs.config1 times the "
+                "CPU port on the same R1CS, z, r, s",
+    }
+    state = {"cs0": cs0, "cs": cs, "z": z, "batch_id": 42, "proof": (proof.a, proof.b, proof.c)}
+    del prover
+    pk.close()
+    return line, state
+
+
 def bench_zbatch(ctx, steps, world, sync_all, allmax):
     """Groth16 proofs/s on the config-4 circuit itself: forge/circuits/
     zelana_batch (MiMC Merkle batch) arithmetized by zelana_amd/zbatch.py and
@@ -688,7 +776,7 @@ def host_cores():
     return cores, {"host_cpus": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "cpu_model": model}
 
 
-def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb_state=None):
+def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb_state=None, c1_state=None):
     """oracle/ restatement of arkworks on this box's host cores, same inputs
     as the GPU legs, each leg checked for equality with the GPU output:
       msm   ark-ec msm_bigint_wnaf on the headline's 2^20 bases / scalars
@@ -765,6 +853,33 @@ def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb
                                     and np.array_equal(c, gc)),
         }
         del keep
+    if c1_state is not None:
+        log("CPU config-1 leg: oracle setup + prove of the small L2 proof")
+        from zelana_amd.rng import StdRng
+        st0, keep0 = O.make_r1cs(c1_state["cs0"])
+        orng = O.Rng(0)  # keygen.rs: StdRng(0); kept alive while setup reads it
+        opk = O.lib().oracle_groth16_setup(ctypes.byref(st0), orng.h, threads)
+        st, keep = O.make_r1cs(c1_state["cs"])
+        zz = np.array([O.int_to_limbs(v) for v in c1_state["z"]], np.uint64)
+        rng = StdRng.seed_from_u64(c1_state["batch_id"])
+        r, s = rng.fr_rand(), rng.fr_rand()
+        rs = np.concatenate([O.int_to_limbs(r), O.int_to_limbs(s)])
+        a, b, c = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+        t0 = time.perf_counter()
+        rc = O.lib().oracle_groth16_prove(opk, ctypes.byref(st), O.P(zz), None, O.P(rs), threads,
+                                          O.P(a), O.P(b), O.P(c), None)
+        dtp = time.perf_counter() - t0
+        O.lib().oracle_pk_free(opk)
+        ga, gb, gc = c1_state["proof"]
+        out["legs"]["config1"] = {
+            "value": round(1.0 / dtp, 2), "unit": "proofs/s", "ms_per_proof": round(dtp * 1e3, 1), "cores": threads,
+            "kind": "port",
+            "sample": f"ark-groth16 prove of the configs[0] L2BlockCircuit proof ({c1_state['cs'].num_constraints} "
+                      "constraints) under the oracle's StdRng(0) key, r and s from StdRng(42); R1CS synthesis excluded",
+            "gpu_matches_cpu": bool(rc == 0 and np.array_equal(a, ga) and np.array_equal(b, gb)
+                                    and np.array_equal(c, gc)),
+        }
+        del keep, keep0, orng
     return out
 
 

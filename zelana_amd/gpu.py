@@ -110,6 +110,7 @@ class Bases:
 class Context:
     def __init__(self, device: int = 0):
         self.h = vp()
+        self.device = device
         check(lib().zkmi_ctx_create(device, ctypes.byref(self.h)), "zkmi_ctx_create")
 
     def close(self):

@@ -1,0 +1,91 @@
+"""ctypes access to the C++ host mirror of the reference prover
+(zelana_amd/libzelana_prover.so: zp::Groth16Prover above the C ABI, with
+L2BlockCircuit synthesis in C++).  This is the native `prove()` surface
+(core/src/sequencer/settlement/prover.rs:350-425) that INTEGRATION.md §4
+describes; bench.py times it for configs[0], tests/test_host_mirror.py checks
+it against the Python mirror."""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+vp, sz = ctypes.c_void_p, ctypes.c_size_t
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        from ._lib import lib as zkmi_lib
+        zkmi_lib()  # libzkmi.so first (libzelana_prover.so links it)
+        L = ctypes.CDLL(os.path.join(HERE, "libzelana_prover.so"))
+        L.zp_last_error.restype = ctypes.c_char_p
+        L.zp_blake3.argtypes = [vp, sz, vp]
+        L.zp_stdrng_fr.argtypes = [ctypes.c_uint64, sz, vp]
+        L.zp_poseidon_hash.argtypes = [vp, sz, vp]
+        L.zp_l2_synthesize.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(vp)]
+        L.zp_r1cs_sizes.argtypes = [vp, vp]
+        L.zp_r1cs_copy.argtypes = [vp, ctypes.c_int, vp, vp, vp]
+        L.zp_r1cs_z.argtypes = [vp, vp]
+        L.zp_r1cs_free.argtypes = [vp]
+        L.zp_groth16_from_bytes.argtypes = [vp, sz, vp, sz, ctypes.c_int, ctypes.POINTER(vp)]
+        L.zp_groth16_prove.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, ctypes.POINTER(ctypes.c_uint64)]
+        L.zp_groth16_vk_hash.argtypes = [vp, vp]
+        L.zp_groth16_free.argtypes = [vp]
+        _L = L
+    return _L
+
+
+def _buf(b: bytes):
+    a = np.frombuffer(bytes(b) or b"\0", np.uint8).copy()
+    return a, a.ctypes.data
+
+
+def encode(inputs, witness):
+    """(BatchPublicInputs, BatchWitness) of zelana_amd.prover -> the capi byte layout."""
+    from .prover import Transfer, Withdraw
+    inp = b"".join(bytes(getattr(inputs, k)) for k in ("pre_state_root", "post_state_root", "pre_shielded_root",
+                                                        "post_shielded_root", "withdrawal_root", "batch_hash"))
+    inp += int(inputs.batch_id).to_bytes(8, "little")
+    tr = [t for t in witness.transactions if isinstance(t, Transfer)]
+    wd = [t for t in witness.transactions if isinstance(t, Withdraw)]
+    trb = b"".join(bytes(t.signer_pubkey) + bytes(t.to) + int(t.amount).to_bytes(8, "little") for t in tr)
+    wdb = b"".join(bytes(32) + bytes(t.to_l1_address) + int(t.amount).to_bytes(8, "little") for t in wd)
+    acb = b"".join(bytes(s.account_id) + int(s.balance).to_bytes(8, "little") for s in witness.pre_account_states)
+    return inp, (trb, len(tr)), (wdb, len(wd)), (acb, len(witness.pre_account_states))
+
+
+class NativeGroth16Prover:
+    """zp::Groth16Prover::from_bytes(pk, vk, device) / prove(inputs, witness)."""
+
+    def __init__(self, pk_bytes: bytes, vk_bytes: bytes, device: int = 0):
+        L = lib()
+        self._pk, self._vk = _buf(pk_bytes), _buf(vk_bytes)
+        self.h = vp()
+        if L.zp_groth16_from_bytes(self._pk[1], len(pk_bytes), self._vk[1], len(vk_bytes), device,
+                                   ctypes.byref(self.h)):
+            raise RuntimeError(L.zp_last_error().decode())
+
+    def prove(self, inputs, witness):
+        """-> (256-B Solana proof bytes, proving_time_ms as the reference reports it)."""
+        L = lib()
+        inp, (trb, nt), (wdb, nw), (acb, na) = encode(inputs, witness)
+        keep = [_buf(inp), _buf(trb), _buf(wdb), _buf(acb)]
+        out = np.zeros(256, np.uint8)
+        ms = ctypes.c_uint64()
+        if L.zp_groth16_prove(self.h, keep[0][1], keep[1][1], nt, keep[2][1], nw, keep[3][1], na, out.ctypes.data,
+                              ctypes.byref(ms)):
+            raise RuntimeError(L.zp_last_error().decode())
+        return out.tobytes(), int(ms.value)
+
+    def close(self):
+        if self.h:
+            lib().zp_groth16_free(self.h)
+            self.h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
