@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--log-n", type=int, default=20, help="points per GPU = 2^log_n")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-table", action="store_true", help="headline without the fixed-base table")
+    ap.add_argument("--inputs", choices=("stdrng", "splitmix"), default="stdrng",
+                    help="MSM input streams: SURVEY.md §8d StdRng streams, or the round-1 splitmix device streams")
     ap.add_argument("--no-plain", action="store_true", help="skip the no-table side measurement")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: every usable core)")
     ap.add_argument("--no-cpu-prove", action="store_true", help="skip the CPU baseline's zelana_batch proof leg")
@@ -106,8 +108,7 @@ def main():
 
         comm = make_comm(ctx, backend)  # libzkmi's own communicator: RCCL, or host (gloo rehearsal)
     n = 1 << args.log_n
-    bases = ctx.bases_generate(seed=1000 + rank, n=n)
-    scalars = ctx.scalars_generate(seed=20 + rank, n=n)
+    bases, scalars = msm_inputs(ctx, args.inputs, 20 + rank, 1020 + rank, n, splitmix_point_seed=1000 + rank)
     dev = torch.device("cuda", gpu_index) if torch.cuda.is_available() else None
     _coll_dev = dev if backend == "nccl" else None  # gloo collectives on host tensors
 
@@ -220,7 +221,7 @@ def main():
     if not args.no_big:
         log("config 5: global 2^%d MSM" % args.big_log_n)
         extra["msm_global_2_%d" % args.big_log_n] = bench_msm_sharded(
-            ctx, args.big_log_n, args.big_steps, world, rank, submit, finish, sync_all, allmax, 2)
+            ctx, args.big_log_n, args.big_steps, world, rank, submit, finish, sync_all, allmax, 2, args.inputs)
     ntt_state = zb_state = None
     if not args.no_ntt:
         log("NTT + INTT")
@@ -267,7 +268,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic (bases k_i*G and uniform Fr scalars generated in HBM)",
+        "data": ("synthetic, SURVEY.md §8d streams: scalars = Fr::rand of StdRng::seed_from_u64(20 + rank), points "
+                 "P_i = P0 + i*D with P0, D = G1::rand of StdRng::seed_from_u64(1020 + rank); resident in HBM"
+                 if args.inputs == "stdrng" else
+                 "synthetic (bases k_i*G and uniform Fr scalars from splitmix streams, generated in HBM)"),
         "config": {
             "workload": f"BN254 G1 MSM, 2^{args.log_n} random scalars/points per GPU (BASELINE.json configs[1]"
                         + (f", sharded across {world} GPUs: global MSM of {world}x2^{args.log_n} points" if world > 1 else "")
@@ -323,7 +327,24 @@ def pipelined(submit, finish, k, depth):
     return res
 
 
-def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_all, allmax, lanes=2):
+def msm_inputs(ctx, kind, scalar_seed, point_seed, n, first=0, splitmix_point_seed=None):
+    """MSM inputs resident in HBM: elements [first, first + n) of the global
+    set.  'stdrng' = SURVEY.md §8d: scalars are Fr::rand draws of
+    StdRng::seed_from_u64(scalar_seed) (C++ zp::StdRng on the host, uploaded),
+    points P_i = P0 + i*D with P0, D the first two G1::rand draws of
+    StdRng::seed_from_u64(point_seed) (generated on the GPU).  'splitmix' =
+    the round-1 device-side streams (k_i*G bases, rejection-sampled scalars)."""
+    if kind == "stdrng":
+        from zelana_amd.host_prover import stdrng_fr, stdrng_g1_stream
+        p0, d = stdrng_g1_stream(point_seed)
+        bases = ctx.bases_arith_g1(p0, d, n, first=first)
+        scalars = ctx.scalars_upload(stdrng_fr(scalar_seed, first + n)[first:])
+        return bases, scalars
+    return (ctx.bases_generate(seed=splitmix_point_seed, n=n, first=first),
+            ctx.scalars_generate(seed=scalar_seed, n=n, first=first))
+
+
+def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_all, allmax, lanes=2, inputs="stdrng"):
     """BASELINE.json configs[4]: ONE global BN254 G1 MSM of 2^log_total
     point-scalar pairs, point-sharded over the world's ranks (strong scaling:
     rank r owns elements [r*N/W, (r+1)*N/W) of the same global set, resident
@@ -337,8 +358,7 @@ def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_a
     total = 1 << log_total
     first, per = shard_range(total, world, rank)
     t0 = time.perf_counter()
-    bases = ctx.bases_generate(seed=1026, n=per, first=first)
-    scalars = ctx.scalars_generate(seed=26, n=per, first=first)
+    bases, scalars = msm_inputs(ctx, inputs, 26, 1026, per, first, splitmix_point_seed=1026)
     gen_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     info = bases.precompute()
@@ -359,7 +379,8 @@ def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_a
     del bases, scalars
     return {
         "workload": f"BN254 G1 MSM 2^{log_total} (BASELINE.json configs[4]): one global MSM point-sharded over "
-                    f"{world} GPU(s), {per} resident points + fixed-base table per GPU; bit sums exchanged by "
+                    f"{world} GPU(s), {per} resident points + fixed-base table per GPU ({inputs} input streams: "
+                    "StdRng(26) scalars, P0 + i*D points from StdRng(1026) for stdrng); bit sums exchanged by "
                     "libzkmi's communicator, group-law sum in its epilogue",
         "value": round(total * steps / dt / 1e6, 2),
         "unit": "Mpoint-scalar/s",

@@ -104,6 +104,11 @@ int zkmi_scalars_generate(zkmi_ctx* ctx, uint64_t seed, size_t n, void* d_scalar
  * [r*n, (r+1)*n) sums to the single-GPU result (multi-GPU bench, config 5). */
 int zkmi_bases_generate_range_g1(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, zkmi_bases** out);
 int zkmi_scalars_generate_range(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, void* d_scalars);
+/* SURVEY.md §8d's point stream: P_i = P0 + (first + i) * D for i < n
+ * (canonical affine P0, D; the bench draws them as G1::rand from
+ * StdRng::seed_from_u64(1020)), generated in HBM. */
+int zkmi_bases_generate_arith_g1(zkmi_ctx* ctx, const uint64_t p0[8], const uint64_t d[8], size_t first, size_t n,
+                                 zkmi_bases** out);
 
 /* sum_{i<n} scalars[i] * bases[offset + i]; n <= len - offset.
  * Host scalars (n x 4 u64). Result: canonical affine. */

@@ -336,3 +336,13 @@ def test_bucket_reduction_mode2_subprocess():
     r = subprocess.run([sys.executable, "-c", _BR_MODE2_SCRIPT, os.path.dirname(here), here], env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_bases_arith_stream_matches_oracle(ctx):
+    """zkmi_bases_generate_arith_g1 (P_i = P0 + (first + i) D in HBM, the
+    bench's §8d point stream) equals the oracle's P0 + i D points."""
+    from zelana_amd.host_prover import stdrng_g1_stream
+    p0, d = stdrng_g1_stream(1020)
+    want = O.gen_points_g1(1020, 1500)
+    assert np.array_equal(ctx.bases_arith_g1(p0, d, 1500).export(), want)
+    assert np.array_equal(ctx.bases_arith_g1(p0, d, 700, first=800).export(), want[800:])

@@ -106,3 +106,18 @@ def test_cpp_groth16_prover_equals_python(tmp_path):
     r = subprocess.run([BIN, "--gpu", str(tmp_path / "pk.bin"), str(tmp_path / "vk.bin")], capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_bench_input_streams_match_oracle():
+    """SURVEY.md §8d's input streams as bench.py draws them (product side:
+    zp::StdRng in libzelana_prover.so, G1::rand in zelana_amd/keygen.py) equal
+    the oracle's: Fr::rand draws of StdRng(20), and P0, D = G1::rand of
+    StdRng(1020) with P_i = P0 + i D."""
+    import oracle_ctypes as O
+    from zelana_amd.host_prover import stdrng_fr, stdrng_g1_stream
+    assert np.array_equal(stdrng_fr(20, 300), O.gen_scalars(20, 300))
+    p0, d = stdrng_g1_stream(1020)
+    pts = O.gen_points_g1(1020, 3)
+    assert np.array_equal(p0, pts[0])
+    two_d = O.msm_g1(np.stack([d]), O.ints_to_array([2]))
+    assert np.array_equal(O.msm_g1(np.stack([p0, d]), O.ints_to_array([1, 2])), pts[2]) and two_d.any()

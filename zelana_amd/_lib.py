@@ -66,6 +66,7 @@ SIGNATURES = [
     ("zkmi_bases_generate_g2", ctypes.c_int, [vp, ctypes.c_uint64, sz, ctypes.POINTER(vp)]),
     ("zkmi_scalars_generate", ctypes.c_int, [vp, ctypes.c_uint64, sz, vp]),
     ("zkmi_bases_generate_range_g1", ctypes.c_int, [vp, ctypes.c_uint64, sz, sz, ctypes.POINTER(vp)]),
+    ("zkmi_bases_generate_arith_g1", ctypes.c_int, [vp, u64p, u64p, sz, sz, ctypes.POINTER(vp)]),
     ("zkmi_scalars_generate_range", ctypes.c_int, [vp, ctypes.c_uint64, sz, sz, vp]),
     ("zkmi_msm_g1", ctypes.c_int, [vp, vp, sz, u64p, sz, u64p]),
     ("zkmi_msm_g2", ctypes.c_int, [vp, vp, sz, u64p, sz, u64p]),

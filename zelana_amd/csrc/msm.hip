@@ -1541,6 +1541,36 @@ __global__ void __launch_bounds__(256) k_gen_bases(uint64_t seed, size_t first, 
     st_fe(q + 24, reduce<FqP>(y.c1));
   }
 }
+// SURVEY.md §8d point stream: P_i = P0 + i * D (P0, D = the first two
+// G1::rand draws of StdRng(seed), drawn on the host), element i of the range
+// = global element first + i.  Canonical affine in, internal affine out.
+__global__ void __launch_bounds__(256) k_gen_bases_arith(const uint32_t* __restrict__ p0d, size_t first, size_t n,
+                                                         uint32_t* __restrict__ out) {
+  using F = FqOps;
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t gi = first + i;
+  Aff<F> p0, d;
+  p0.x = to_mont<FqP>(ld_fe(p0d));
+  p0.y = to_mont<FqP>(ld_fe(p0d + 8));
+  d.x = to_mont<FqP>(ld_fe(p0d + 16));
+  d.y = to_mont<FqP>(ld_fe(p0d + 24));
+  Xyzz<F> acc = xyzz_inf<F>();
+  for (int b = 63; b >= 0; b--) {
+    acc = xyzz_dbl(acc);
+    if ((gi >> b) & 1) acc = xyzz_madd(acc, d);
+  }
+  acc = xyzz_madd(acc, p0);
+  uint32_t* q = out + i * G1T::PW;
+  if (xyzz_is_inf(acc)) {  // P0 + i D = O: stored as the infinity flag
+    for (int k = 0; k < G1T::PW; k++) q[k] = 0;
+    q[G1T::PW - 1] = 1u << 31;
+    return;
+  }
+  Fe izz = fq_inv(acc.zz), izzz = fq_inv(acc.zzz);
+  st_fe(q, reduce<FqP>(mul<FqP>(acc.x, izz)));
+  st_fe(q + 8, reduce<FqP>(mul<FqP>(acc.y, izzz)));
+}
 // Fixed-base table: copy j of point i is 2^(shift) * copy (j-1), in affine
 // form (one inversion of ZZ*ZZZ per copy).  Built once per base set (pk load);
 // MSMs then trade W windows of n entries for Wp windows of p*n entries, which
@@ -1730,6 +1760,33 @@ int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t first, size_t n,
   zkmi_bases* b = new zkmi_bases;
   b->ctx = ctx;
   b->g2 = g2;
+  b->n = n;
+  b->d_pts = d_pts;
+  *out = b;
+  return 0;
+}
+int bases_generate_arith_g1(zkmi_ctx* ctx, const uint64_t p0[8], const uint64_t d[8], size_t first, size_t n,
+                            zkmi_bases** out) {
+  uint32_t* d_pts = nullptr;
+  uint32_t* d_in = nullptr;
+  if (hipMalloc(&d_pts, std::max<size_t>(1, n) * 64) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("hipMalloc(%zu) failed for bases", n * 64);
+    return ZKMI_ENOMEM;
+  }
+  ZK_TRY(ctx->ws.get("bases_arith_in", 128, (void**)&d_in));
+  uint64_t h[16];
+  memcpy(h, p0, 64);
+  memcpy(h + 8, d, 64);
+  ZK_HIP(hipMemcpyAsync(d_in, h, 128, hipMemcpyHostToDevice, ctx->stream));
+  if (n) {
+    k_gen_bases_arith<<<(unsigned)((n + 255) / 256), 256, 0, ctx->stream>>>(d_in, first, n, d_pts);
+    ZK_HIP(hipGetLastError());
+  }
+  ZK_HIP(hipStreamSynchronize(ctx->stream));
+  zkmi_bases* b = new zkmi_bases;
+  b->ctx = ctx;
+  b->g2 = 0;
   b->n = n;
   b->d_pts = d_pts;
   *out = b;

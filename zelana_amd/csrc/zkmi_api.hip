@@ -282,6 +282,15 @@ int zkmi_bases_generate_range_g1(zkmi_ctx* ctx, uint64_t seed, size_t first, siz
   ZK_DEVICE_GUARD(ctx);
   return bases_generate(ctx, 0, seed, first, n, out);
 }
+int zkmi_bases_generate_arith_g1(zkmi_ctx* ctx, const uint64_t p0[8], const uint64_t d[8], size_t first, size_t n,
+                                 zkmi_bases** out) {
+  ZK_DEVICE_GUARD(ctx);
+  if (!ctx || !p0 || !d || !out) {
+    set_error("zkmi_bases_generate_arith_g1: null argument");
+    return ZKMI_EINVAL;
+  }
+  return bases_generate_arith_g1(ctx, p0, d, first, n, out);
+}
 int zkmi_scalars_generate_range(zkmi_ctx* ctx, uint64_t seed, size_t first, size_t n, void* d_scalars) {
   ZK_DEVICE_GUARD(ctx);
   return scalars_generate(ctx, seed, first, n, d_scalars);

@@ -179,6 +179,8 @@ int bases_from_device_canon(zkmi_ctx* ctx, int g2, const uint32_t* d_canon, size
 
 // synthetic inputs generated in HBM (bench) and canonical export (checks)
 int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t first, size_t n, zkmi_bases** out);
+int bases_generate_arith_g1(zkmi_ctx* ctx, const uint64_t p0[8], const uint64_t d[8], size_t first, size_t n,
+                            zkmi_bases** out);
 inline int bases_generate(zkmi_ctx* ctx, int g2, uint64_t seed, size_t n, zkmi_bases** out) {
   return bases_generate(ctx, g2, seed, 0, n, out);
 }

@@ -161,6 +161,25 @@ class Context:
         """Synthetic bases k_i*G generated in HBM; elements [first, first+n) of seed's set."""
         return Bases(self, None, g2, generate_seed=seed, n=n, first=first)
 
+    def bases_arith_g1(self, p0, d, n: int, first: int = 0):
+        """Bases P_i = P0 + (first + i) * D generated in HBM (SURVEY.md §8d's
+        point stream; P0, D canonical affine, 8 u64 each)."""
+        b = Bases.__new__(Bases)
+        b.ctx, b.g2, b.n, b.h = self, False, n, vp()
+        p0 = np.ascontiguousarray(p0, np.uint64)
+        d = np.ascontiguousarray(d, np.uint64)
+        check(lib().zkmi_bases_generate_arith_g1(self.h, _p64(p0), _p64(d), first, n, ctypes.byref(b.h)),
+              "zkmi_bases_generate_arith_g1")
+        return b
+
+    def scalars_upload(self, scalars: np.ndarray) -> DeviceBuffer:
+        """(n, 4) canonical u64 scalars into a device buffer."""
+        sc = np.ascontiguousarray(scalars, np.uint64).reshape(-1, 4)
+        buf = DeviceBuffer(self, max(1, sc.shape[0]) * 32)
+        if sc.shape[0]:
+            buf.upload(sc)
+        return buf
+
     def scalars_generate(self, seed: int, n: int, first: int = 0) -> DeviceBuffer:
         buf = DeviceBuffer(self, max(1, n) * 32)
         check(lib().zkmi_scalars_generate_range(self.h, seed, first, n, buf.ptr), "zkmi_scalars_generate_range")

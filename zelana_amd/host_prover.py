@@ -56,6 +56,24 @@ def encode(inputs, witness):
     return inp, (trb, len(tr)), (wdb, len(wd)), (acb, len(witness.pre_account_states))
 
 
+def stdrng_fr(seed: int, k: int) -> np.ndarray:
+    """The first k Fr::rand draws of StdRng::seed_from_u64(seed), canonical
+    (k, 4) u64 (C++ ChaCha12 + arkworks rejection sampling, zp::StdRng)."""
+    out = np.zeros((max(k, 1), 4), np.uint64)
+    lib().zp_stdrng_fr(seed, k, out.ctypes.data)
+    return out[:k]
+
+
+def stdrng_g1_stream(seed: int):
+    """(P0, D): the first two G1::rand draws of StdRng::seed_from_u64(seed),
+    canonical affine 8 x u64 each (SURVEY.md §8d config 2/5 point stream)."""
+    from .keygen import _limbs, g1_rand
+    from .rng import StdRng
+    rng = StdRng.seed_from_u64(seed)
+    p0, d = g1_rand(rng), g1_rand(rng)
+    return (np.array(_limbs(p0[0]) + _limbs(p0[1]), np.uint64), np.array(_limbs(d[0]) + _limbs(d[1]), np.uint64))
+
+
 class NativeGroth16Prover:
     """zp::Groth16Prover::from_bytes(pk, vk, device) / prove(inputs, witness)."""
 
