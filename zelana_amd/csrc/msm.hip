@@ -2248,7 +2248,7 @@ static BrGeom br_geom(const MsmPlan& P, bool g2) {
   BrGeom g;
   g.mode = P.hb >= 9 ? (env_mode == 2 ? 2 : 1) : 0;
   g.S = env_fold == 4 ? 4 : 8;
-  g.segt = 256;
+  g.segt = env_seg == 64 || env_seg == 128 ? env_seg : 256;
   if (g.mode == 2) {
     g.sr = g.sc = 1;
     g.segt = env_seg == 64 || env_seg == 256 ? env_seg : 128;
