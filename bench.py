@@ -251,7 +251,9 @@ def main():
                 "sq_insts_valu_per_launch": pmc.get("sq_insts_valu"),
                 "achieved_G_wave_instr_per_s": round(pmc["sq_insts_valu"] / kavg_s / 1e9, 1)
                 if pmc.get("sq_insts_valu") and kcnt else None,
-                "pmc_clock_ghz": pmc.get("clock_ghz"),
+                # dispatch cycles (GRBM_GUI_ACTIVE / 8, PMC pass) over this run's isolated kernel time
+                "effective_clock_ghz": round(pmc["dispatch_cycles"] / kavg_s / 1e9, 3)
+                if pmc.get("dispatch_cycles") and kcnt else None,
                 "note": "the bound that applies: fraction of the 1024 SIMDs' cycles issuing VALU work, "
                         "SQ_ACTIVE_INST_VALU x 4 / (1024 x GRBM_GUI_ACTIVE / 8), both counted on the same "
                         "dispatches (no assumed clock or cycle cost); from the committed profiles/pmc_traffic.json "
