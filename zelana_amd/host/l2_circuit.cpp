@@ -99,19 +99,34 @@ const PoseidonParams& poseidon_params() {  // find_poseidon_ark_and_mds(254, 2, 
 
 // ------------------------------------------------------------------ CS
 constexpr uint64_t kWit = 1ULL << 62;  // witness symbols; instance k -> k, One = 0
-using LC = std::map<uint64_t, Fr>;
+// A linear combination: terms sorted by symbol (what a std::map held before;
+// one merge per addition instead of a node allocation per term -- the
+// Poseidon partial rounds' growing combinations made that the synthesis's
+// cost).  Coefficients that cancel stay as zero terms, which the matrix
+// conversion skips, as it did with the map.
+using LC = std::vector<std::pair<uint64_t, Fr>>;
 
 LC lc_add(const LC& a, const LC& b, bool sub = false) {
-  LC o = a;
-  for (const auto& kv : b) {
-    Fr& t = o[kv.first];
-    t = sub ? t - kv.second : t + kv.second;
+  LC o;
+  o.reserve(a.size() + b.size());
+  size_t i = 0, j = 0;
+  while (i < a.size() || j < b.size()) {
+    if (j == b.size() || (i < a.size() && a[i].first < b[j].first)) {
+      o.push_back(a[i++]);
+    } else if (i == a.size() || b[j].first < a[i].first) {
+      o.emplace_back(b[j].first, sub ? Fr() - b[j].second : b[j].second);
+      j++;
+    } else {
+      o.emplace_back(a[i].first, sub ? a[i].second - b[j].second : a[i].second + b[j].second);
+      i++, j++;
+    }
   }
   return o;
 }
 LC lc_scale(const LC& a, const Fr& c) {
   LC o;
-  for (const auto& kv : a) o[kv.first] = kv.second * c;
+  o.reserve(a.size());
+  for (const auto& kv : a) o.emplace_back(kv.first, kv.second * c);
   return o;
 }
 
