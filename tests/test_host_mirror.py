@@ -121,3 +121,25 @@ def test_bench_input_streams_match_oracle():
     assert np.array_equal(p0, pts[0])
     two_d = O.msm_g1(np.stack([d]), O.ints_to_array([2]))
     assert np.array_equal(O.msm_g1(np.stack([p0, d]), O.ints_to_array([1, 2])), pts[2]) and two_d.any()
+
+
+@pytest.mark.parametrize("k", [0, 2])
+def test_native_synthesizer_wrapper(k):
+    """zelana_amd.host_prover.native_l2_block_circuit (what Groth16Prover.prove
+    synthesizes with when libzelana_prover.so is built) returns the Python
+    restatement's matrices (per-row term order aside) and z."""
+    from zelana_amd.host_prover import native_l2_block_circuit
+    from zelana_amd.prover import _as_z, l2_block_circuit
+    inputs, witness = _batches()[k]
+    cs1, z1 = native_l2_block_circuit(inputs, witness)
+    cs2, z2 = l2_block_circuit(inputs, witness)
+    assert (cs1.num_constraints, cs1.num_instance, cs1.num_witness) == \
+        (cs2.num_constraints, cs2.num_instance, cs2.num_witness)
+    assert np.array_equal(z1, _as_z(z2))
+    for name in "abc":
+        (rp, col, val), (prp, pcol, pval) = cs1.csr(name), cs2.csr(name)
+        assert np.array_equal(rp, prp)
+        for r in range(cs1.num_constraints):
+            got = sorted((int(col[q]), tuple(val[q].tolist())) for q in range(rp[r], rp[r + 1]))
+            want = sorted((int(pcol[q]), tuple(pval[q].tolist())) for q in range(prp[r], prp[r + 1]))
+            assert got == want

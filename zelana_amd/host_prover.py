@@ -74,6 +74,39 @@ def stdrng_g1_stream(seed: int):
     return (np.array(_limbs(p0[0]) + _limbs(p0[1]), np.uint64), np.array(_limbs(d[0]) + _limbs(d[1]), np.uint64))
 
 
+def native_l2_block_circuit(inputs, witness):
+    """(R1CS, z) of L2BlockCircuit for (inputs, witness), synthesized by the C++
+    host mirror (zp L2BlockCircuit::synthesize): the same matrices and
+    assignment as zelana_amd.prover.l2_block_circuit
+    (tests/test_host_mirror.py::test_cpp_synthesis_equals_python), ~30x faster.
+    The R1CS carries CSR arrays only (no row lists)."""
+    from .r1cs import R1CS
+    L = lib()
+    inp, (trb, nt), (wdb, nw), (acb, na) = encode(inputs, witness)
+    keep = [_buf(inp), _buf(trb), _buf(wdb), _buf(acb)]
+    h = vp()
+    if L.zp_l2_synthesize(keep[0][1], keep[1][1], nt, keep[2][1], nw, keep[3][1], na, ctypes.byref(h)):
+        raise RuntimeError(L.zp_last_error().decode())
+    try:
+        sizes = np.zeros(7, np.uint64)
+        L.zp_r1cs_sizes(h, sizes.ctypes.data)
+        m, ni, nwit = (int(x) for x in sizes[:3])
+        cs = R1CS(ni, nwit)
+        cs._m = m
+        for t, name in enumerate("abc"):
+            nnz = int(sizes[3 + t])
+            rp = np.zeros(m + 1, np.uint64)
+            col = np.zeros(max(nnz, 1), np.uint64)
+            val = np.zeros((max(nnz, 1), 4), np.uint64)
+            L.zp_r1cs_copy(h, t, rp.ctypes.data, col.ctypes.data, val.ctypes.data)
+            cs.set_csr(name, rp, col, val)
+        z = np.zeros((ni + nwit, 4), np.uint64)
+        L.zp_r1cs_z(h, z.ctypes.data)
+    finally:
+        L.zp_r1cs_free(h)
+    return cs, z
+
+
 class NativeGroth16Prover:
     """zp::Groth16Prover::from_bytes(pk, vk, device) / prove(inputs, witness)."""
 

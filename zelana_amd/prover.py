@@ -123,7 +123,7 @@ class Groth16Prover:
         self.pk = pk
         self.verifying_key = vk_bytes
         self.vk_hash = blake3(vk_bytes)
-        self.circuit = circuit if circuit is not None else l2_block_circuit
+        self.circuit = circuit if circuit is not None else default_l2_synthesizer()
 
     @classmethod
     def from_bytes(cls, pk_bytes: bytes, vk_bytes: bytes, device: int = 0, circuit=None, compressed=True,
@@ -209,6 +209,22 @@ class Groth16Prover:
 
     def export_vk_json(self) -> str:
         return json.dumps({"verifying_key": base64.b64encode(self.verifying_key).decode()}, indent=2)
+
+
+def default_l2_synthesizer():
+    """L2BlockCircuit synthesis for Groth16Prover.prove: the C++ host mirror
+    (zelana_amd/host_prover.py, identical matrices and z, ~30x faster) when
+    libzelana_prover.so is built, else the Python restatement;
+    ZKMI_PY_SYNTH=1 forces the Python one."""
+    import os
+    if os.environ.get("ZKMI_PY_SYNTH") != "1":
+        try:
+            from .host_prover import lib as _hlib, native_l2_block_circuit
+            _hlib()
+            return native_l2_block_circuit
+        except OSError:
+            pass
+    return l2_block_circuit
 
 
 def _as_z(z):
