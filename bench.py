@@ -615,8 +615,9 @@ def bench_config1(ctx, steps=5):
         "resident_proof_equal": same,
         "native_prove_ms": round(g_nat * 1e3, 2), "native_proof_equal": nbytes == proof.proof_bytes,
         "note": "native_prove_ms = zp::Groth16Prover::prove (libzelana_prover.so: C++ synthesis + libzkmi), the "
-                "drop-in surface; ms_per_proof = the Python mirror's prove() (its Python R1CS synthesis and CSR "
-                "conversion dominate); gpu_prove_ms = the same R1CS and z through zkmi_groth16_prove (CSR + z uploaded per call), "
+                "drop-in surface; ms_per_proof = the Python mirror's prove() (synthesis through the same C++ "
+                "synthesizer, CSR uploaded per call); host_synthesis_ms = the Python restatement's synthesis alone; "
+                "gpu_prove_ms = the same R1CS and z through zkmi_groth16_prove (CSR + z uploaded per call), "
                 "gpu_prove_resident_ms = through zkmi_groth16_prove_resident; cpu_baseline.legs.config1 times the "
                 "CPU port on the same R1CS, z, r, s",
     }
