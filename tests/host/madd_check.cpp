@@ -1,6 +1,7 @@
 // Host build of the device field/curve code (ff.h / ec.h are host+device):
 // the lazy G1 mixed addition xyzz_madd_g1 must give the same group element
-// as the reference-form xyzz_madd over long accumulation chains, including
+// as the reference-form xyzz_madd over long accumulation chains (and so must
+// the msm.hip acc_step rule: second point by the affine + affine xyzz_mmadd_*), including
 // P == Q, P == -Q, lazy X inputs and negated bases.  Prints "ok <n>".
 #include <stdio.h>
 #include <stdlib.h>
@@ -84,7 +85,19 @@ static int check_g2() {
   }
   int checks = 0;
   for (int trial = 0; trial < 60; trial++) {
-    Xyzz<F2> a = xyzz_inf<F2>(), b = xyzz_inf<F2>();
+    Xyzz<F2> a = xyzz_inf<F2>(), b = xyzz_inf<F2>(), c = xyzz_inf<F2>();
+    bool naff = false;
+    auto step = [&](const Aff<F2>& q) {
+      if (xyzz_is_inf(c)) {
+        c = xyzz_from_aff(q);
+        naff = true;
+      } else if (naff) {
+        c = xyzz_mmadd_g2({c.x, c.y}, q);
+        naff = false;
+      } else {
+        c = xyzz_madd_g2(c, q);
+      }
+    };
     int len = 1 + (int)(next() % 24), prev = -1;
     for (int s = 0; s < len; s++) {
       int j = (int)(next() % NP);
@@ -96,23 +109,31 @@ static int check_g2() {
       qb.y = {fq_cneg(qb.y.c0, neg_), fq_cneg(qb.y.c1, neg_)};
       a = xyzz_madd(a, qa);
       b = xyzz_madd_g2(b, qb);
+      step(qb);
       if (mode == 1) {
         Aff<F2> na = qa, nb = pts[j];
         na.y = f2_neg(qa.y);
         nb.y = {fq_cneg(nb.y.c0, !neg_), fq_cneg(nb.y.c1, !neg_)};
         a = xyzz_madd(a, na);
         b = xyzz_madd_g2(b, nb);
+        step(nb);
       }
       prev = j;
-      if (!same2(a, b)) {
+      if (!same2(a, b) || !same2(a, c)) {
         printf("G2 mismatch trial %d step %d\n", trial, s);
         return -1;
       }
       checks++;
     }
     Aff<F2> q = pts[trial % NP];
-    if (!same2(xyzz_madd_g2(xyzz_from_aff(q), q), xyzz_mdbl(q))) {
+    if (!same2(xyzz_madd_g2(xyzz_from_aff(q), q), xyzz_mdbl(q)) || !same2(xyzz_mmadd_g2(q, q), xyzz_mdbl(q))) {
       printf("G2 doubling mismatch\n");
+      return -1;
+    }
+    Aff<F2> nq = q, w = pts[(trial + 1) % NP];
+    nq.y = {fq_cneg(q.y.c0, true), fq_cneg(q.y.c1, true)};
+    if (!xyzz_is_inf(xyzz_mmadd_g2(q, nq)) || !same2(xyzz_mmadd_g2(q, w), xyzz_madd(xyzz_from_aff(q), w))) {
+      printf("G2 mmadd mismatch\n");
       return -1;
     }
   }
@@ -137,7 +158,19 @@ int main() {
   }
   int checks = 0;
   for (int trial = 0; trial < 200; trial++) {
-    Xyzz<F> a = xyzz_inf<F>(), b = xyzz_inf<F>();
+    Xyzz<F> a = xyzz_inf<F>(), b = xyzz_inf<F>(), c = xyzz_inf<F>();
+    bool naff = false;  // msm.hip acc_step: first point as is, second by xyzz_mmadd_g1
+    auto step = [&](const Aff<F>& q) {
+      if (xyzz_is_inf(c)) {
+        c = xyzz_from_aff(q);
+        naff = true;
+      } else if (naff) {
+        c = xyzz_mmadd_g1({c.x, c.y}, q);
+        naff = false;
+      } else {
+        c = xyzz_madd_g1(c, q);
+      }
+    };
     int len = 1 + (int)(next() % 40);
     int prev = -1;
     for (int s = 0; s < len; s++) {
@@ -152,15 +185,17 @@ int main() {
       qb.y = fq_cneg(q.y, neg_);
       a = xyzz_madd(a, qa);
       b = xyzz_madd_g1(b, qb);
+      step(qb);
       if (mode == 1) {  // cancel: add -Q right after Q
         Aff<F> na = qa, nb = q;
         na.y = neg<FqP>(qa.y);
         nb.y = fq_cneg(q.y, !neg_);
         a = xyzz_madd(a, na);
         b = xyzz_madd_g1(b, nb);
+        step(nb);
       }
       prev = j;
-      if (!same(a, b)) {
+      if (!same(a, b) || !same(a, c)) {
         printf("mismatch trial %d step %d\n", trial, s);
         return 1;
       }
@@ -176,6 +211,14 @@ int main() {
     n.y = fq_cneg(n.y, true);
     if (!xyzz_is_inf(xyzz_madd_g1(xyzz_from_aff(pts[trial % NP]), n))) {
       printf("cancel mismatch\n");
+      return 1;
+    }
+    // affine + affine: doubling, cancellation, and the generic case
+    const Aff<F>& u = pts[trial % NP];
+    const Aff<F>& w = pts[(trial + 1) % NP];
+    if (!same(xyzz_mmadd_g1(u, u), xyzz_mdbl(u)) || !xyzz_is_inf(xyzz_mmadd_g1(u, n)) ||
+        !same(xyzz_mmadd_g1(u, w), xyzz_madd(xyzz_from_aff(u), w))) {
+      printf("mmadd mismatch\n");
       return 1;
     }
   }

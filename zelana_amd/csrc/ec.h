@@ -142,6 +142,55 @@ ZK_HD Xyzz<FqOps> xyzz_madd_g1(const Xyzz<FqOps>& p, const Aff<FqOps>& q) {
   r.zzz = mul<FqP>(p.zzz, ppp);
   return r;
 }
+// P + Q with both affine (mmadd-2008-s): xyzz_madd_g1 with ZZ1 = ZZZ1 = 1, so
+// U2 = x2, S2 = y2, ZZ3 = PP, ZZZ3 = PPP -- four products fewer (the second
+// entry of every bucket; the first is xyzz_from_aff).  Same field values as
+// xyzz_madd_g1(xyzz_from_aff(p), q).  In: p, q < 2p.  Out: as xyzz_madd_g1.
+ZK_HD Xyzz<FqOps> xyzz_mmadd_g1(const Aff<FqOps>& p, const Aff<FqOps>& q) {
+  Fe pp_ = subk<FqP, 2>(q.x, p.x);        // x2 - x1 + 2p   in (0, 4p)
+  Fe ny1 = subk<FqP, 2>(fe_zero(), p.y);  // 2p - y1        in (0, 2p]
+  Fe rr = add_lazy(q.y, ny1);             // y2 - y1 + 2p   < 4p, limbs < 2^30
+  Fe pp = sqr<FqP>(pp_);
+  if (is_zero<FqP>(pp)) {
+    Fe rn = reduce8<FqP>(subk<FqP, 2>(q.y, p.y));
+    if (is_zero<FqP>(rn)) return xyzz_mdbl(q);
+    return xyzz_inf<FqOps>();
+  }
+  Fe ppp = mul<FqP>(pp_, pp);
+  Fe qq = mul<FqP>(p.x, pp);
+  Fe t = add_lazy(add_lazy(ppp, qq), qq);
+  Xyzz<FqOps> r;
+  r.x = subk<FqP, 6>(sqr<FqP>(rr), t);
+  Fe qx = subk<FqP, 8>(qq, r.x);
+  r.y = mul2<FqP>(rr, qx, ny1, ppp);
+  r.zz = pp;
+  r.zzz = ppp;
+  return r;
+}
+// Fq2 counterpart of xyzz_mmadd_g1 (four Fq2 products fewer than
+// xyzz_madd_g2).  In: p, q < 2p.  Out: as xyzz_madd_g2.
+ZK_HD Xyzz<Fq2Ops> xyzz_mmadd_g2(const Aff<Fq2Ops>& p, const Aff<Fq2Ops>& q) {
+  Fe2 pp_ = {subk<FqP, 2>(q.x.c0, p.x.c0), subk<FqP, 2>(q.x.c1, p.x.c1)};  // (0, 4p)
+  Fe2 rr = {subk<FqP, 2>(q.y.c0, p.y.c0), subk<FqP, 2>(q.y.c1, p.y.c1)};   // (0, 4p)
+  Fe2 pp = f2_sqr_n(pp_);
+  if (f2_is_zero(pp)) {
+    if (is_zero<FqP>(reduce8<FqP>(rr.c0)) && is_zero<FqP>(reduce8<FqP>(rr.c1))) return xyzz_mdbl(q);
+    return xyzz_inf<Fq2Ops>();
+  }
+  Fe2 r2 = f2_sqr_n(rr);
+  Fe2 ppp = f2_mul_n(pp_, pp), qq = f2_mul_n(p.x, pp);
+  Xyzz<Fq2Ops> r;
+  r.x.c0 = reduce8<FqP>(subk<FqP, 6>(r2.c0, add_lazy(add_lazy(ppp.c0, qq.c0), qq.c0)));
+  r.x.c1 = reduce8<FqP>(subk<FqP, 6>(r2.c1, add_lazy(add_lazy(ppp.c1, qq.c1), qq.c1)));
+  Fe2 qx = {subk<FqP, 2>(qq.c0, r.x.c0), subk<FqP, 2>(qq.c1, r.x.c1)};  // (0, 4p)
+  Fe ny0 = subk<FqP, 2>(fe_zero(), p.y.c0), ny1 = subk<FqP, 2>(fe_zero(), p.y.c1);
+  Fe nqx1 = subk<FqP, 4>(fe_zero(), qx.c1), nppp1 = subk<FqP, 2>(fe_zero(), ppp.c1);
+  r.y.c0 = mul4<FqP>(rr.c0, qx.c0, rr.c1, nqx1, ny0, ppp.c0, ny1, nppp1);
+  r.y.c1 = mul4<FqP>(rr.c0, qx.c1, rr.c1, qx.c0, ny0, ppp.c1, ny1, ppp.c0);
+  r.zz = pp;
+  r.zzz = ppp;
+  return r;
+}
 // G2 (Fq2) counterpart: lazy single-pass subtractions, Fq2 products with one
 // reduction per component, Y3 as two four-product passes.  X stays < 2p here
 // (Fq2 squares of lazy sums would leave the 169 p^2 product bound).

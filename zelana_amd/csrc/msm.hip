@@ -96,6 +96,28 @@ __device__ __forceinline__ void st_xyzz(uint32_t* p, const Xyzz<typename G::F>& 
   Io<F>::st(p + 3 * G::CW, v.zzz);
 }
 
+#ifndef ZK_MMADD
+#define ZK_MMADD 1
+#endif
+// One bucket-accumulation step acc += P.  The first point of a run is taken
+// as is and the second one added by the affine + affine form (four products
+// fewer than the mixed addition); `naff` tracks "acc is exactly one affine
+// point".  Lanes of a wave run equal trip counts, so the branches are uniform.
+template <class G>
+__device__ __forceinline__ void acc_step(Xyzz<typename G::F>& acc, bool& naff, const Aff<typename G::F>& P) {
+  if (xyzz_is_inf(acc)) {
+    acc = xyzz_from_aff(P);
+    naff = true;
+  } else if (ZK_MMADD && naff) {
+    if constexpr (G::CW == 8) acc = xyzz_mmadd_g1({acc.x, acc.y}, P);
+    else acc = xyzz_mmadd_g2({acc.x, acc.y}, P);
+    naff = false;
+  } else {
+    if constexpr (G::CW == 8) acc = xyzz_madd_g1(acc, P);
+    else acc = xyzz_madd_g2(acc, P);
+  }
+}
+
 // Curve addition of the reductions (piece sums, cascade, bucket reduction).
 // (Split-column products for these 1-2 waves/SIMD kernels -- four independent
 // accumulators per column -- measured no faster: 2^20 lines kernel 217 -> 195
@@ -938,6 +960,7 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
   };
   constexpr bool PF = G::CW == 8;  // G2: see msm_acc0_body
   Xyzz<F> acc = xyzz_inf<F>();
+  bool naff = false;  // acc is one affine point (ZZ = ZZZ = 1)
   uint32_t v_nxt = sval[start];
   uint4 raw[PQ];
   if constexpr (PF) {
@@ -970,12 +993,11 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
     if constexpr (G::CW == 8) {
       P.x = unpack(w);
       P.y = fq_cneg(unpack(w + 8), v >> 31);
-      acc = xyzz_madd_g1(acc, P);
     } else {
       P.x = {unpack(w), unpack(w + 8)};
       P.y = {fq_cneg(unpack(w + 16), v >> 31), fq_cneg(unpack(w + 24), v >> 31)};
-      acc = xyzz_madd_g2(acc, P);
     }
+    acc_step<G>(acc, naff, P);
   }
   if (it.w == NOSLOT) {
     st_acc<G>(buckets + (size_t)it.z * XW, acc);
