@@ -15,10 +15,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 name = sys.argv[1] if len(sys.argv) > 1 else "k_acc_items_g1"
-out = "/tmp/zkmi_isa/msm.s"
+SRC = os.environ.get("SRC", "msm")
+out = f"/tmp/zkmi_isa/{SRC}.s"
 os.makedirs(os.path.dirname(out), exist_ok=True)
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "--cuda-device-only", "-S",
-                "-o", out, os.path.join(ROOT, "zelana_amd", "csrc", "msm.hip")] + sys.argv[2:], check=True)
+                "-o", out, os.path.join(ROOT, "zelana_amd", "csrc", SRC + ".hip")] + sys.argv[2:], check=True)
 s = open(out).read()
 m = re.search(r"^(_Z[^\s:]*" + re.escape(name) + r"[^\s:]*):", s, re.M)
 if not m:

@@ -57,6 +57,13 @@ struct FrP {
                                      0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
   static constexpr uint32_t P2[NL] = {0x00000002u, 0x1e1f593fu, 0x1cb848a1u, 0x0fa121e6u, 0x0b0ba506u,
                                       0x05b68181u, 0x014dc282u, 0x1cb84c68u, 0x0060c89cu};
+  // 4r, 6r, 8r (biases of the lazy subtractions, conditional subtractions)
+  static constexpr uint32_t P4[NL] = {0x00000004u, 0x1c3eb27eu, 0x19709143u, 0x1f4243cdu, 0x16174a0cu,
+                                      0x0b6d0302u, 0x029b8504u, 0x197098d0u, 0x00c19139u};
+  static constexpr uint32_t P6[NL] = {0x00000006u, 0x1a5e0bbdu, 0x1628d9e5u, 0x0ee365b4u, 0x0122ef13u,
+                                      0x11238484u, 0x03e94786u, 0x1628e538u, 0x012259d6u};
+  static constexpr uint32_t P8[NL] = {0x00000008u, 0x187d64fcu, 0x12e12287u, 0x1e84879bu, 0x0c2e9419u,
+                                      0x16da0605u, 0x05370a08u, 0x12e131a0u, 0x01832273u};
   static constexpr uint32_t PINV = 0x0fffffffu;
   static constexpr uint32_t ONE[NL] = {0x0fffff57u, 0x1ea70ab4u, 0x052c068bu, 0x17504f49u, 0x0aa8075bu,
                                        0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};

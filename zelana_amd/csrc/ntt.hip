@@ -102,19 +102,52 @@ struct NttGroup {
   }
 };
 
-// u - v + 2r in one signed-carry pass, u, v in [0, 2r): a multiplier input
-// in (0, 4r), which the Montgomery product absorbs (4r * r << 169 r^2).
-__device__ __forceinline__ Fe fr_sub_lazy(const Fe& a, const Fe& b) {
-  Fe r;
-  int32_t c = 0;
+// Lazy DIF sums.  A DIF butterfly's sum x0 = u + v needs no reduction until
+// the round's elements are stored: x0 is a limb-wise add (9 ops instead of two
+// carry chains), and the difference takes a bias K r >= v in one signed-carry
+// pass before its multiplication.  Every element carries a bound (value < b r,
+// limbs < l 2^29) that is a compile-time constant per register slot (the
+// stage loops are unrolled), so the bias choice and the end-of-round
+// reduction to [0, 2r) fold away.  Bounds: b <= 16 (the sub output stays
+// < 24 r, far inside the Montgomery product's 169 r^2), limbs < 2^32 unsigned
+// and < 2^31 wherever a signed-carry pass reads them.
+template <int K>
+__device__ __forceinline__ Fe fr_csub(const Fe& x) {  // x - K r if that is >= 0, else x
+  const uint32_t* kp = K == 2 ? FrP::P2 : K == 4 ? FrP::P4 : FrP::P8;
+  Fe d;
+  int32_t br = 0;
 #pragma unroll
   for (int i = 0; i < NL; i++) {
-    int32_t t = (int32_t)(a.v[i] + FrP::P2[i]) - (int32_t)b.v[i] + c;
-    r.v[i] = (uint32_t)t & LMASK;
-    c = t >> 29;
+    int32_t t = (int32_t)x.v[i] - (int32_t)kp[i] + br;
+    d.v[i] = (uint32_t)t & LMASK;
+    br = t >> 29;
   }
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = br < 0 ? x.v[i] : d.v[i];
   return r;
 }
+// carry-propagate limbs < 2^31 into 29-bit limbs (the top limb keeps the rest)
+__device__ __forceinline__ Fe fr_norm(const Fe& x) {
+  Fe r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    const uint32_t t = x.v[i] + c;
+    r.v[i] = t & LMASK;
+    c = t >> 29;
+  }
+  r.v[NL - 1] = x.v[NL - 1] + c;
+  return r;
+}
+// value < b r, normalised limbs -> [0, 2r)
+__device__ __forceinline__ Fe fr_reduce_from(Fe x, int b) {
+  if (b > 8) x = fr_csub<8>(x);
+  if (b > 4) x = fr_csub<4>(x);
+  if (b > 2) x = fr_csub<2>(x);
+  return x;
+}
+__device__ __forceinline__ int fr_pow2_ceil(int b) { return b <= 2 ? 2 : b <= 4 ? 4 : b <= 8 ? 8 : 16; }
 
 // TRIV: the round touches stages whose twiddles are omega^0 for every pair p
 // with p mod 2^rb == 0 (the register round at tile bit lsub of a group with
@@ -124,6 +157,12 @@ template <bool DIT, int R, bool TRIV, int EPT>
 __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint32_t lo, const uint32_t* __restrict__ tw,
                                               const NttGroup& g) {
   constexpr int NP = EPT / 2;  // butterflies per stage per thread
+  int bd[EPT], lb[EPT];          // DIF bounds per slot (see fr_csub)
+#pragma unroll
+  for (int t = 0; t < EPT; t++) {
+    bd[t] = 2;
+    lb[t] = 1;
+  }
 #pragma unroll
   for (int si = 0; si < R; si++) {
     const int rb = DIT ? si : R - 1 - si;  // register bit of this stage
@@ -145,20 +184,47 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint3
     for (int p = 0; p < NP; p++) {
       const int t0 = ((p >> rb) << (rb + 1)) | (p & ((1 << rb) - 1)), t1 = t0 | (1 << rb);
       Fe u = x[t0], v = x[t1];
-      if (TRIV && (p & ((1 << rb) - 1)) == 0) {
-        x[t0] = add<FrP>(u, v);
-        x[t1] = sub<FrP>(u, v);
-        continue;
-      }
-      const Fe wp = w[p];
+      const bool one_w = TRIV && (p & ((1 << rb) - 1)) == 0;
       if (DIT) {
-        Fe t = mul<FrP>(v, wp);
+        if (one_w) {
+          x[t0] = add<FrP>(u, v);
+          x[t1] = sub<FrP>(u, v);
+          continue;
+        }
+        Fe t = mul<FrP>(v, w[p]);
         x[t0] = add<FrP>(u, t);
         x[t1] = sub<FrP>(u, t);
       } else {
-        x[t0] = add<FrP>(u, v);
-        x[t1] = mul<FrP>(fr_sub_lazy(u, v), wp);
+        if (lb[t0] > 3) {  // the signed-carry pass below reads u's limbs
+          u = fr_norm(u);
+          lb[t0] = 1;
+        }
+        const int bu = bd[t0], bv = fr_pow2_ceil(bd[t1]);
+        Fe dlt;
+        if (bv == 2) dlt = subk<FrP, 2>(u, v);
+        else if (bv == 4) dlt = subk<FrP, 4>(u, v);
+        else dlt = subk<FrP, 8>(u, v);
+        Fe sum = add_lazy(u, v);
+        int ls = lb[t0] + lb[t1];
+        if (ls > 4) {
+          sum = fr_norm(sum);
+          ls = 1;
+        }
+        x[t0] = sum;
+        bd[t0] = bu + bd[t1];
+        lb[t0] = ls;
+        x[t1] = one_w ? dlt : mul<FrP>(dlt, w[p]);
+        bd[t1] = one_w ? bu + bv : 2;
+        lb[t1] = 1;
       }
+    }
+  }
+  if (!DIT) {  // back to normalised [0, 2r) for LDS / HBM
+#pragma unroll
+    for (int t = 0; t < EPT; t++) {
+      Fe v = x[t];
+      if (lb[t] > 1) v = fr_norm(v);
+      x[t] = fr_reduce_from(v, bd[t]);
     }
   }
 }
