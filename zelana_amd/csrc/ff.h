@@ -64,6 +64,8 @@ struct FrP {
                                       0x11238484u, 0x03e94786u, 0x1628e538u, 0x012259d6u};
   static constexpr uint32_t P8[NL] = {0x00000008u, 0x187d64fcu, 0x12e12287u, 0x1e84879bu, 0x0c2e9419u,
                                       0x16da0605u, 0x05370a08u, 0x12e131a0u, 0x01832273u};
+  static constexpr uint32_t P16[NL] = {0x00000010u, 0x10fac9f8u, 0x05c2450fu, 0x1d090f37u, 0x185d2833u,
+                                       0x0db40c0au, 0x0a6e1411u, 0x05c26340u, 0x030644e7u};
   static constexpr uint32_t PINV = 0x0fffffffu;
   static constexpr uint32_t ONE[NL] = {0x0fffff57u, 0x1ea70ab4u, 0x052c068bu, 0x17504f49u, 0x0aa8075bu,
                                        0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};

@@ -113,7 +113,7 @@ struct NttGroup {
 // and < 2^31 wherever a signed-carry pass reads them.
 template <int K>
 __device__ __forceinline__ Fe fr_csub(const Fe& x) {  // x - K r if that is >= 0, else x
-  const uint32_t* kp = K == 2 ? FrP::P2 : K == 4 ? FrP::P4 : FrP::P8;
+  const uint32_t* kp = K == 2 ? FrP::P2 : K == 4 ? FrP::P4 : K == 8 ? FrP::P8 : FrP::P16;
   Fe d;
   int32_t br = 0;
 #pragma unroll
@@ -141,13 +141,39 @@ __device__ __forceinline__ Fe fr_norm(const Fe& x) {
   return r;
 }
 // value < b r, normalised limbs -> [0, 2r)
+__device__ __forceinline__ Fe fr_reduce_q32(const Fe& x);
 __device__ __forceinline__ Fe fr_reduce_from(Fe x, int b) {
-  if (b > 8) x = fr_csub<8>(x);
-  if (b > 4) x = fr_csub<4>(x);
+  if (b > 4) return fr_reduce_q32(x);  // b <= 32
   if (b > 2) x = fr_csub<2>(x);
   return x;
 }
+// value < 32 r, normalised limbs -> [0, 2r) with one quotient-estimate
+// subtraction instead of four conditional ones: q = floor(x8 * M / 2^48),
+// M = floor(2^48 / (r8 + 2)) (x8, r8 the top limbs), satisfies
+// x / r - 1 - 2^-14 < q <= x / r, so x - q r lies in [0, 2r).
+__device__ __forceinline__ Fe fr_reduce_q32(const Fe& x) {
+  constexpr uint32_t M = 88753946u;  // floor(2^48 / (0x30644e + 2))
+  const uint32_t q = (uint32_t)(((uint64_t)x.v[NL - 1] * M) >> 48);
+  Fe r;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const int64_t t = (int64_t)x.v[i] - (int64_t)((uint64_t)q * FrP::P[i]) + c;
+    r.v[i] = (uint32_t)t & LMASK;
+    c = t >> 29;
+  }
+  return r;
+}
 __device__ __forceinline__ int fr_pow2_ceil(int b) { return b <= 2 ? 2 : b <= 4 ? 4 : b <= 8 ? 8 : 16; }
+
+// Lazy DIT sums.  A DIT butterfly adds 2r to the bound of both outputs (x0 =
+// u + t, x1 = u - t + 2r, with t = v w < 2r), so the growth over a pass is
+// additive: values stay normalised at round ends (LDS) and are reduced once,
+// on the pass's last round.  The omega^0 round (round 0 of the innermost
+// group, inputs < 2r from HBM) doubles its bounds instead; with <= 8 stages a
+// pass ends below 16 + 5 * 2 = 26 r, and one quotient-estimate subtraction
+// (fr_reduce_q32) brings it to [0, 2r).  v enters the product < 32 r.
+constexpr int NTT_DIT_BOUND = 32;
 
 // TRIV: the round touches stages whose twiddles are omega^0 for every pair p
 // with p mod 2^rb == 0 (the register round at tile bit lsub of a group with
@@ -186,14 +212,38 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint3
       Fe u = x[t0], v = x[t1];
       const bool one_w = TRIV && (p & ((1 << rb) - 1)) == 0;
       if (DIT) {
-        if (one_w) {
-          x[t0] = add<FrP>(u, v);
-          x[t1] = sub<FrP>(u, v);
+        if (lb[t0] > 3) {  // the signed-carry pass below reads u's limbs
+          u = fr_norm(u);
+          lb[t0] = 1;
+        }
+        if (one_w) {  // round 0 only: bd[] are the true bounds here
+          const int bu = bd[t0], bvt = bd[t1], bv = fr_pow2_ceil(bvt);
+          Fe dlt;
+          if (bv == 2) dlt = subk<FrP, 2>(u, v);
+          else if (bv == 4) dlt = subk<FrP, 4>(u, v);
+          else dlt = subk<FrP, 8>(u, v);
+          Fe sum = add_lazy(u, v);
+          int ls = lb[t0] + lb[t1];
+          if (ls > 4) {
+            sum = fr_norm(sum);
+            ls = 1;
+          }
+          x[t1] = dlt;
+          bd[t1] = bu + bv;
+          lb[t1] = 1;
+          x[t0] = sum;
+          bd[t0] = bu + bvt;
+          lb[t0] = ls;
           continue;
         }
-        Fe t = mul<FrP>(v, w[p]);
-        x[t0] = add<FrP>(u, t);
-        x[t1] = sub<FrP>(u, t);
+        if (lb[t1] > 2) v = fr_norm(v);  // product operand limbs < 2^30
+        const Fe t = mul<FrP>(v, w[p]);
+        x[t1] = subk<FrP, 2>(u, t);
+        bd[t1] = bd[t0] + 2;
+        lb[t1] = 1;
+        x[t0] = add_lazy(u, t);
+        bd[t0] += 2;
+        lb[t0] += 1;
       } else {
         if (lb[t0] > 3) {  // the signed-carry pass below reads u's limbs
           u = fr_norm(u);
@@ -226,6 +276,10 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint3
       if (lb[t] > 1) v = fr_norm(v);
       x[t] = fr_reduce_from(v, bd[t]);
     }
+  } else {  // normalised for LDS; k_ntt_group reduces on the pass's last round
+#pragma unroll
+    for (int t = 0; t < EPT; t++)
+      if (lb[t] > 1) x[t] = fr_norm(x[t]);
   }
 }
 
@@ -320,6 +374,7 @@ __global__ void __launch_bounds__(256, (RB == 3 ? 2 : 4)) k_ntt_group(const uint
 #pragma unroll
       for (int t = 0; t < EPT; t++) {
         const size_t gi = g.gidx(base | ((uint32_t)t << lo));
+        if (DIT) x[t] = fr_reduce_q32(x[t]);  // lazy DIT sums (< NTT_DIT_BOUND r) -> [0, 2r)
         if (EPI == 0 && !PERM) {
           st_fe(dst + gi * 8, x[t]);
         } else {
