@@ -130,6 +130,17 @@ static int check_g2() {
       printf("G2 doubling mismatch\n");
       return -1;
     }
+    {
+      Xyzz<F2> other = xyzz_madd(xyzz_madd(xyzz_inf<F2>(), pts[(trial + 3) % NP]), pts[(trial + 5) % NP]);
+      Xyzz<F2> neg_a = a;
+      neg_a.y = f2_neg(a.y);
+      if (!same2(xyzz_add_g2(a, other), xyzz_add(a, other)) || !same2(xyzz_add_g2(a, a), xyzz_add(a, a)) ||
+          !xyzz_is_inf(xyzz_add_g2(a, neg_a)) != !xyzz_is_inf(xyzz_add(a, neg_a)) ||
+          !same2(xyzz_add_g2(xyzz_inf<F2>(), other), other)) {
+        printf("G2 full add mismatch trial %d\n", trial);
+        return -1;
+      }
+    }
     Aff<F2> nq = q, w = pts[(trial + 1) % NP];
     nq.y = {fq_cneg(q.y.c0, true), fq_cneg(q.y.c1, true)};
     if (!xyzz_is_inf(xyzz_mmadd_g2(q, nq)) || !same2(xyzz_mmadd_g2(q, w), xyzz_madd(xyzz_from_aff(q), w))) {
@@ -212,6 +223,19 @@ int main() {
     if (!xyzz_is_inf(xyzz_madd_g1(xyzz_from_aff(pts[trial % NP]), n))) {
       printf("cancel mismatch\n");
       return 1;
+    }
+    // full additions (bucket reductions): lazy form vs the generic formula,
+    // on chain values with non-trivial ZZ, including P + P and P + (-P)
+    {
+      Xyzz<F> other = xyzz_madd(xyzz_madd(xyzz_inf<F>(), pts[(trial + 3) % NP]), pts[(trial + 5) % NP]);
+      Xyzz<F> neg_a = a;
+      neg_a.y = neg<FqP>(a.y);
+      if (!same(xyzz_add_g1(a, other), xyzz_add(a, other)) || !same(xyzz_add_g1(a, a), xyzz_add(a, a)) ||
+          !xyzz_is_inf(xyzz_add_g1(a, neg_a)) != !xyzz_is_inf(xyzz_add(a, neg_a)) ||
+          !same(xyzz_add_g1(xyzz_inf<F>(), other), other) || !same(xyzz_add_g1(other, xyzz_inf<F>()), other)) {
+        printf("full add mismatch trial %d\n", trial);
+        return 1;
+      }
     }
     // affine + affine: doubling, cancellation, and the generic case
     const Aff<F>& u = pts[trial % NP];

@@ -220,6 +220,68 @@ ZK_HD Xyzz<Fq2Ops> xyzz_madd_g2(const Xyzz<Fq2Ops>& p, const Aff<Fq2Ops>& q) {
   return r;
 }
 
+// P + Q with both in XYZZ (add-2008-s) in the lazy forms of xyzz_madd_g1:
+// U1/S1 take the place of X1/Y1, Y3 is one two-product pass, and X3 is
+// brought back to [0, 2p) so the contract is xyzz_add's (the bucket
+// reductions store and exchange these points).  In/out: coordinates < 2p,
+// normalised.
+ZK_HD Xyzz<FqOps> xyzz_add_g1(const Xyzz<FqOps>& p, const Xyzz<FqOps>& q) {
+  if (xyzz_is_inf(p)) return q;
+  if (xyzz_is_inf(q)) return p;
+  Fe u1 = mul<FqP>(p.x, q.zz);
+  Fe u2 = mul<FqP>(q.x, p.zz);
+  Fe s1 = mul<FqP>(p.y, q.zzz);
+  Fe s2 = mul<FqP>(q.y, p.zzz);
+  Fe pp_ = subk<FqP, 2>(u2, u1);          // U2 - U1 + 2p   in (0, 4p)
+  Fe ny1 = subk<FqP, 2>(fe_zero(), s1);   // 2p - S1        in (0, 2p]
+  Fe rr = add_lazy(s2, ny1);              // S2 - S1 + 2p   < 4p, limbs < 2^30
+  Fe pp = sqr<FqP>(pp_);
+  if (is_zero<FqP>(pp)) {
+    Fe rn = reduce8<FqP>(subk<FqP, 2>(s2, s1));
+    if (is_zero<FqP>(rn)) return xyzz_dbl(p);
+    return xyzz_inf<FqOps>();
+  }
+  Fe ppp = mul<FqP>(pp_, pp);
+  Fe qq = mul<FqP>(u1, pp);
+  Fe t = add_lazy(add_lazy(ppp, qq), qq);  // PPP + 2Q < 6p, limbs < 3*2^29
+  Xyzz<FqOps> r;
+  Fe x = subk<FqP, 6>(sqr<FqP>(rr), t);    // in (0, 8p)
+  Fe qx = subk<FqP, 8>(qq, x);             // Q - X3 + 8p in (0, 10p)
+  r.y = mul2<FqP>(rr, qx, ny1, ppp);       // R (Q - X3) - S1 PPP
+  r.x = reduce8<FqP>(x);
+  r.zz = mul<FqP>(mul<FqP>(p.zz, q.zz), pp);
+  r.zzz = mul<FqP>(mul<FqP>(p.zzz, q.zzz), ppp);
+  return r;
+}
+// Fq2 counterpart (the products of xyzz_madd_g2: one reduction per component).
+// In/out: coordinates < 2p, normalised.
+ZK_HD Xyzz<Fq2Ops> xyzz_add_g2(const Xyzz<Fq2Ops>& p, const Xyzz<Fq2Ops>& q) {
+  if (xyzz_is_inf(p)) return q;
+  if (xyzz_is_inf(q)) return p;
+  Fe2 u1 = f2_mul_n(p.x, q.zz), u2 = f2_mul_n(q.x, p.zz);
+  Fe2 s1 = f2_mul_n(p.y, q.zzz), s2 = f2_mul_n(q.y, p.zzz);
+  Fe2 pp_ = {subk<FqP, 2>(u2.c0, u1.c0), subk<FqP, 2>(u2.c1, u1.c1)};  // (0, 4p)
+  Fe2 rr = {subk<FqP, 2>(s2.c0, s1.c0), subk<FqP, 2>(s2.c1, s1.c1)};   // (0, 4p)
+  Fe2 pp = f2_sqr_n(pp_);
+  if (f2_is_zero(pp)) {
+    if (is_zero<FqP>(reduce8<FqP>(rr.c0)) && is_zero<FqP>(reduce8<FqP>(rr.c1))) return xyzz_dbl(p);
+    return xyzz_inf<Fq2Ops>();
+  }
+  Fe2 r2 = f2_sqr_n(rr);
+  Fe2 ppp = f2_mul_n(pp_, pp), qq = f2_mul_n(u1, pp);
+  Xyzz<Fq2Ops> r;
+  r.x.c0 = reduce8<FqP>(subk<FqP, 6>(r2.c0, add_lazy(add_lazy(ppp.c0, qq.c0), qq.c0)));
+  r.x.c1 = reduce8<FqP>(subk<FqP, 6>(r2.c1, add_lazy(add_lazy(ppp.c1, qq.c1), qq.c1)));
+  Fe2 qx = {subk<FqP, 2>(qq.c0, r.x.c0), subk<FqP, 2>(qq.c1, r.x.c1)};  // (0, 4p)
+  Fe ny0 = subk<FqP, 2>(fe_zero(), s1.c0), ny1 = subk<FqP, 2>(fe_zero(), s1.c1);
+  Fe nqx1 = subk<FqP, 4>(fe_zero(), qx.c1), nppp1 = subk<FqP, 2>(fe_zero(), ppp.c1);
+  r.y.c0 = mul4<FqP>(rr.c0, qx.c0, rr.c1, nqx1, ny0, ppp.c0, ny1, nppp1);
+  r.y.c1 = mul4<FqP>(rr.c0, qx.c1, rr.c1, qx.c0, ny0, ppp.c1, ny1, ppp.c0);
+  r.zz = f2_mul_n(f2_mul_n(p.zz, q.zz), pp);
+  r.zzz = f2_mul_n(f2_mul_n(p.zzz, q.zzz), ppp);
+  return r;
+}
+
 // conditional negation of an affine y (< 2p) without a borrow/fix-up pass
 ZK_HD Fe fq_cneg(const Fe& y, bool neg_) {
   Fe n = subk<FqP, 2>(fe_zero(), y);

@@ -122,9 +122,16 @@ __device__ __forceinline__ void acc_step(Xyzz<typename G::F>& acc, bool& naff, c
 // (Split-column products for these 1-2 waves/SIMD kernels -- four independent
 // accumulators per column -- measured no faster: 2^20 lines kernel 217 -> 195
 // us, bit sums 139 -> 143 us; dropped.)
+// The lazy-form additions (ec.h xyzz_add_g1/g2) issue ~15-25% fewer VALU
+// instructions than the generic xyzz_add; ZK_BR_GENERIC=1 keeps the latter.
+#ifndef ZK_BR_GENERIC
+#define ZK_BR_GENERIC 0
+#endif
 template <class G>
 __device__ __forceinline__ Xyzz<typename G::F> br_add(const Xyzz<typename G::F>& p, const Xyzz<typename G::F>& q) {
-  return xyzz_add(p, q);
+  if constexpr (ZK_BR_GENERIC) return xyzz_add(p, q);
+  else if constexpr (G::CW == 8) return xyzz_add_g1(p, q);
+  else return xyzz_add_g2(p, q);
 }
 
 // ----------------------------------------------------------------- digits
