@@ -151,7 +151,49 @@ static int check_g2() {
   return checks;
 }
 
+// reduce_q32 (one-pass [0, 32p) -> [0, 2p)) on x = k p + e for every k < 32,
+// e in {0, 1, p - 1, random}: the result is < 2p and congruent to e.
+template <class P>
+static bool check_reduce_q32() {
+  for (uint32_t k = 0; k < 32; k++) {
+    for (int kind = 0; kind < 8; kind++) {
+      Fe e = fe_zero();
+      if (kind == 1) e.v[0] = 1;
+      if (kind == 2) {  // p - 1
+        e = fe_const<P>(P::P);
+        e.v[0] -= 1;
+      }
+      if (kind >= 3) {  // random < p: random limbs, top limb below p's
+        for (int i = 0; i < NL; i++) e.v[i] = (uint32_t)next() & LMASK;
+        e.v[NL - 1] %= P::P[NL - 1];
+      }
+      Fe x;
+      uint64_t c = 0;
+      for (int i = 0; i < NL; i++) {
+        uint64_t t = (uint64_t)k * P::P[i] + e.v[i] + c;
+        x.v[i] = (uint32_t)t & LMASK;
+        c = t >> 29;
+      }
+      x.v[NL - 1] += (uint32_t)(c << 29);
+      Fe r = reduce_q32<P>(x);
+      Fe two = fe_const<P>(P::P2);
+      // r < 2p: compare from the top limb
+      int cmp = 0;
+      for (int i = NL - 1; i >= 0 && !cmp; i--) cmp = r.v[i] < two.v[i] ? -1 : r.v[i] > two.v[i] ? 1 : 0;
+      Fe a = reduce<P>(r), b = reduce<P>(e);
+      bool same_ = true;
+      for (int i = 0; i < NL; i++) same_ = same_ && a.v[i] == b.v[i] && r.v[i] <= LMASK;
+      if (cmp >= 0 || !same_) {
+        printf("reduce_q32 mismatch k=%u kind=%d\n", k, kind);
+        return false;
+      }
+    }
+  }
+  return true;
+}
+
 int main() {
+  if (!check_reduce_q32<FqP>() || !check_reduce_q32<FrP>()) return 1;
   Aff<F> g;
   g.x = to_mont<FqP>(Fe{{1, 0, 0, 0, 0, 0, 0, 0, 0}});
   g.y = to_mont<FqP>(Fe{{2, 0, 0, 0, 0, 0, 0, 0, 0}});

@@ -458,26 +458,29 @@ ZK_HD Fe mul4(const Fe& a, const Fe& b, const Fe& c, const Fe& d, const Fe& e, c
   return r;
 }
 
+// [0, 32p) -> [0, 2p), normalised limbs, in one pass (Fq and Fr share the
+// top limb p8 = 0x30644e): q = floor(x8 M / 2^48), M = floor(2^48 / (p8 + 2)),
+// satisfies x / p - 1 - 2^-14 < q <= x / p (x8 < 2^27), so x - q p is in
+// [0, 2p).  One 9-limb signed-carry pass instead of conditional subtractions.
+template <class P>
+ZK_HD Fe reduce_q32(const Fe& x) {
+  static_assert(P::P[NL - 1] == 0x0030644eu, "top limb of the quotient estimate");
+  constexpr uint32_t M = 88753946u;  // floor(2^48 / (0x30644e + 2))
+  const uint32_t q = (uint32_t)(((uint64_t)x.v[NL - 1] * M) >> 48);
+  Fe r;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const int64_t t = (int64_t)x.v[i] - (int64_t)((uint64_t)q * P::P[i]) + c;
+    r.v[i] = (uint32_t)t & LMASK;
+    c = t >> 29;
+  }
+  return r;
+}
 // [0, 8p) -> [0, 2p), normalised limbs
 template <class P>
 ZK_HD Fe reduce8(const Fe& a) {
-  Fe x = a;
-#pragma unroll
-  for (int step = 0; step < 2; step++) {
-    const uint32_t* kp = step == 0 ? P::P4 : P::P2;
-    Fe d;
-    int32_t br = 0;
-#pragma unroll
-    for (int i = 0; i < NL; i++) {
-      int32_t t = (int32_t)x.v[i] - (int32_t)kp[i] + br;
-      d.v[i] = (uint32_t)t & LMASK;
-      br = t >> 29;
-    }
-    const bool neg_ = br < 0;
-#pragma unroll
-    for (int i = 0; i < NL; i++) x.v[i] = neg_ ? x.v[i] : d.v[i];
-  }
-  return x;
+  return reduce_q32<P>(a);
 }
 
 // fully reduce [0, 2p) -> [0, p)

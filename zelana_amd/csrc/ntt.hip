@@ -147,23 +147,8 @@ __device__ __forceinline__ Fe fr_reduce_from(Fe x, int b) {
   if (b > 2) x = fr_csub<2>(x);
   return x;
 }
-// value < 32 r, normalised limbs -> [0, 2r) with one quotient-estimate
-// subtraction instead of four conditional ones: q = floor(x8 * M / 2^48),
-// M = floor(2^48 / (r8 + 2)) (x8, r8 the top limbs), satisfies
-// x / r - 1 - 2^-14 < q <= x / r, so x - q r lies in [0, 2r).
-__device__ __forceinline__ Fe fr_reduce_q32(const Fe& x) {
-  constexpr uint32_t M = 88753946u;  // floor(2^48 / (0x30644e + 2))
-  const uint32_t q = (uint32_t)(((uint64_t)x.v[NL - 1] * M) >> 48);
-  Fe r;
-  int64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const int64_t t = (int64_t)x.v[i] - (int64_t)((uint64_t)q * FrP::P[i]) + c;
-    r.v[i] = (uint32_t)t & LMASK;
-    c = t >> 29;
-  }
-  return r;
-}
+// value < 32 r, normalised limbs -> [0, 2r) in one pass (ff.h reduce_q32)
+__device__ __forceinline__ Fe fr_reduce_q32(const Fe& x) { return reduce_q32<FrP>(x); }
 __device__ __forceinline__ int fr_pow2_ceil(int b) { return b <= 2 ? 2 : b <= 4 ? 4 : b <= 8 ? 8 : 16; }
 
 // Lazy DIT sums.  A DIT butterfly adds 2r to the bound of both outputs (x0 =
