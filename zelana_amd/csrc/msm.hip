@@ -917,9 +917,20 @@ __global__ void k_items_offsets(const uint32_t* __restrict__ hist, uint32_t cap,
   *nitems = run;
 }
 
+// Also resets the partial list the segmented cascade reads (xkey = no key,
+// xvalid = 0) -- only when k_items_count found a bucket the cascade must
+// finish (open_flag); otherwise no cascade level reads the list.
 __global__ void __launch_bounds__(256) k_items_scatter(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
                                                        const uint32_t* __restrict__ pbase,
-                                                       uint32_t* __restrict__ cursor, uint4* __restrict__ items) {
+                                                       uint32_t* __restrict__ cursor, uint4* __restrict__ items,
+                                                       const uint32_t* __restrict__ open_flag, uint32_t* __restrict__ xkey,
+                                                       uint32_t* __restrict__ xvalid, uint32_t xl) {
+  if (*open_flag) {
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < xl; i += (size_t)gridDim.x * 256) {
+      xkey[i] = 0xFFFFFFFFu;
+      xvalid[i] = 0;
+    }
+  }
   __shared__ uint32_t lc[ITEM_CAP_MAX + 1], lbase[ITEM_CAP_MAX + 1];
   for (uint32_t i = threadIdx.x; i <= cap; i += 256) lc[i] = 0;
   __syncthreads();
@@ -1035,11 +1046,12 @@ template <class G>
 __global__ void __launch_bounds__(256) k_items_combine(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
                                                        const uint32_t* __restrict__ pbase,
                                                        uint32_t* __restrict__ buckets, uint32_t* __restrict__ xvalid,
-                                                       const uint32_t* __restrict__ xpts) {
+                                                       const uint32_t* __restrict__ xpts,
+                                                       const uint32_t* __restrict__ npieces) {
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= K) return;
+  if (b >= K || *npieces == 0) return;  // no bucket was split (uniform data: the usual case)
   const uint32_t size = bstart[b + 1] - bstart[b];
   const uint32_t np = (size + cap - 1) / cap;
   if (np < 2 || np > ITEM_SEQ_MAX) return;
@@ -2361,8 +2373,6 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     ZK_TRY(ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
     ZK_TRY(ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
     ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
-    ZK_HIP(hipMemsetAsync(xkey, 0xFF, xl * 4, st));
-    ZK_HIP(hipMemsetAsync(xvalid, 0, xl * 4, st));
     if (!((debug_skip() & 1) && lane->debug_sorted == 2)) {
       lane->debug_sorted = 2;
       ScopedKernelTimer tm(ctx, "msm_items_plan", st);
@@ -2370,7 +2380,8 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       k_items_count<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hist, hv, &flags[0]);
       scan_excl(st, hv, K, bsums, &nitems[1]);
       k_items_offsets<<<1, 1, 0, st>>>(hist, cap, cursor, &nitems[0]);
-      k_items_scatter<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, cursor, items);
+      k_items_scatter<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, cursor, items, &flags[0], xkey, xvalid,
+                                                       (uint32_t)xl);
     }
     {
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
@@ -2379,7 +2390,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
                                                                xkey, xvalid, xpts);
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);
-    k_items_combine<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, buckets, xvalid, xpts);
+    k_items_combine<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, buckets, xvalid, xpts, &nitems[1]);
     ZK_HIP(hipGetLastError());
   } else {
     // level 0: fixed-size chunks of the sorted list (sized from the upper bound
