@@ -741,7 +741,7 @@ def bench_zbatch(ctx, steps, world, sync_all, allmax):
     zstride = (z.nbytes + 255) // 256 * 256
     zsets = [gpu.DeviceBuffer(ctx, NB * zstride) for _ in range(2)]
     zviews = [[zs.view(k * zstride, z.nbytes) for k in range(NB)] for zs in zsets]
-    groups = max(2, (2 * steps + NB - 1) // NB)
+    groups = max(4, (8 * steps + NB - 1) // NB)  # 16 groups at the default 8 steps: the first group's witness is the only one not hidden
     ctx.sync()
     t0 = time.perf_counter()
     for _ in range(steps):
