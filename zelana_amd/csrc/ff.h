@@ -462,6 +462,9 @@ ZK_HD Fe mul4(const Fe& a, const Fe& b, const Fe& c, const Fe& d, const Fe& e, c
 // top limb p8 = 0x30644e): q = floor(x8 M / 2^48), M = floor(2^48 / (p8 + 2)),
 // satisfies x / p - 1 - 2^-14 < q <= x / p (x8 < 2^27), so x - q p is in
 // [0, 2p).  One 9-limb signed-carry pass instead of conditional subtractions.
+// The input's limbs 0..7 may be unnormalised (< 2^31, e.g. limb-wise sums):
+// they move the value by < 4 units of the top limb, which only lowers q by a
+// vanishing fraction, and the carry pass normalises the output.
 template <class P>
 ZK_HD Fe reduce_q32(const Fe& x) {
   static_assert(P::P[NL - 1] == 0x0030644eu, "top limb of the quotient estimate");

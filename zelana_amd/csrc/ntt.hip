@@ -108,25 +108,12 @@ struct NttGroup {
 // pass before its multiplication.  Every element carries a bound (value < b r,
 // limbs < l 2^29) that is a compile-time constant per register slot (the
 // stage loops are unrolled), so the bias choice and the end-of-round
-// reduction to [0, 2r) fold away.  Bounds: b <= 16 (the sub output stays
-// < 24 r, far inside the Montgomery product's 169 r^2), limbs < 2^32 unsigned
-// and < 2^31 wherever a signed-carry pass reads them.
-template <int K>
-__device__ __forceinline__ Fe fr_csub(const Fe& x) {  // x - K r if that is >= 0, else x
-  const uint32_t* kp = K == 2 ? FrP::P2 : K == 4 ? FrP::P4 : K == 8 ? FrP::P8 : FrP::P16;
-  Fe d;
-  int32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    int32_t t = (int32_t)x.v[i] - (int32_t)kp[i] + br;
-    d.v[i] = (uint32_t)t & LMASK;
-    br = t >> 29;
-  }
-  Fe r;
-#pragma unroll
-  for (int i = 0; i < NL; i++) r.v[i] = br < 0 ? x.v[i] : d.v[i];
-  return r;
-}
+// reduction to [0, 2r) fold away: slots above 2r take one quotient-estimate
+// pass (fr_reduce_q32, which also normalises), the others at most a carry
+// pass.  Bounds: b <= 16 (the sub output stays < 24 r, far inside the
+// Montgomery product's 169 r^2), limbs < 2^31 wherever a signed-carry pass
+// reads them.
+//
 // carry-propagate limbs < 2^31 into 29-bit limbs (the top limb keeps the rest)
 __device__ __forceinline__ Fe fr_norm(const Fe& x) {
   Fe r;
@@ -140,14 +127,7 @@ __device__ __forceinline__ Fe fr_norm(const Fe& x) {
   r.v[NL - 1] = x.v[NL - 1] + c;
   return r;
 }
-// value < b r, normalised limbs -> [0, 2r)
-__device__ __forceinline__ Fe fr_reduce_q32(const Fe& x);
-__device__ __forceinline__ Fe fr_reduce_from(Fe x, int b) {
-  if (b > 4) return fr_reduce_q32(x);  // b <= 32
-  if (b > 2) x = fr_csub<2>(x);
-  return x;
-}
-// value < 32 r, normalised limbs -> [0, 2r) in one pass (ff.h reduce_q32)
+// value < 32 r (limbs < 2^31) -> [0, 2r), normalised, in one pass (ff.h reduce_q32)
 __device__ __forceinline__ Fe fr_reduce_q32(const Fe& x) { return reduce_q32<FrP>(x); }
 __device__ __forceinline__ int fr_pow2_ceil(int b) { return b <= 2 ? 2 : b <= 4 ? 4 : b <= 8 ? 8 : 16; }
 
@@ -168,7 +148,7 @@ template <bool DIT, int R, bool TRIV, int EPT>
 __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint32_t lo, const uint32_t* __restrict__ tw,
                                               const NttGroup& g) {
   constexpr int NP = EPT / 2;  // butterflies per stage per thread
-  int bd[EPT], lb[EPT];          // DIF bounds per slot (see fr_csub)
+  int bd[EPT], lb[EPT];          // bounds per slot (see "Lazy DIF sums")
 #pragma unroll
   for (int t = 0; t < EPT; t++) {
     bd[t] = 2;
@@ -257,9 +237,8 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint3
   if (!DIT) {  // back to normalised [0, 2r) for LDS / HBM
 #pragma unroll
     for (int t = 0; t < EPT; t++) {
-      Fe v = x[t];
-      if (lb[t] > 1) v = fr_norm(v);
-      x[t] = fr_reduce_from(v, bd[t]);
+      if (bd[t] > 2) x[t] = fr_reduce_q32(x[t]);  // also normalises limbs < 2^31
+      else if (lb[t] > 1) x[t] = fr_norm(x[t]);
     }
   } else {  // normalised for LDS; k_ntt_group reduces on the pass's last round
 #pragma unroll
