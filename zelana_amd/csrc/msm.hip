@@ -1271,8 +1271,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
 template <class G>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br_strip(const uint32_t* __restrict__ buckets,
                                                       const uint32_t* __restrict__ bstart, int lb, int hb, int W,
-                                                      int sr, int sc, uint32_t* __restrict__ outC,
+                                                      int sr, int sc, int mc, uint32_t* __restrict__ outC,
                                                       uint32_t* __restrict__ outD) {
+  // mc = lanes per column line (a power of two <= 64): 64 / mc columns share
+  // a wave, so a short column gets the same fold length as a row and a
+  // shallower tree (2^19 buckets: 512-bucket columns, mc = 32 -> 16 folds +
+  // 5 levels per lane instead of 8 + 6, 25% fewer wave-additions there).
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   __shared__ Xyzz<F> sh[4][32];
@@ -1280,33 +1284,40 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t job = blockIdx.x * 4 + wave;
   const uint32_t nrow = ((uint32_t)W << hb) * sr, ncol = ((uint32_t)W << lb) * sc;
-  const bool live = job < nrow + ncol;
+  const uint32_t cpw = 64u / (uint32_t)mc;  // column lines per wave
+  const bool row_wave = job < nrow;
+  const uint32_t m = row_wave ? 64u : (uint32_t)mc;  // lanes per line (wave-uniform)
+  const uint32_t sub = lane & (m - 1), lslot = (lane / m) * (m / 2);
+  bool live = false;
   uint32_t len = 0, stride = 1, bucket0 = 0;
   uint32_t* dst = nullptr;
-  if (live) {
-    if (job < nrow) {  // segment g of row h of window w (C[h][g], as k_msm_br)
-      const uint32_t rh = job / sr, g = job % sr, w = rh >> hb, h = rh & ((1u << hb) - 1);
-      len = (1u << lb) / sr;
-      bucket0 = (w << bb) + (h << lb) + g * len;
-      stride = 1;
-      dst = outC + (size_t)job * XW;
-    } else {  // segment g of column l of window w
-      const uint32_t jj = job - nrow, cl = jj / sc, g = jj % sc, w = cl >> lb, l = cl & ((1u << lb) - 1);
+  if (row_wave) {  // segment g of row h of window w (C[h][g], as k_msm_br)
+    const uint32_t rh = job / sr, g = job % sr, w = rh >> hb, h = rh & ((1u << hb) - 1);
+    live = true;
+    len = (1u << lb) / sr;
+    bucket0 = (w << bb) + (h << lb) + g * len;
+    stride = 1;
+    dst = outC + (size_t)job * XW;
+  } else {  // segment g of column l of window w
+    const uint32_t jj = (job - nrow) * cpw + lane / m;
+    if (jj < ncol) {
+      const uint32_t cl = jj / sc, g = jj % sc, w = cl >> lb, l = cl & ((1u << lb) - 1);
+      live = true;
       len = (1u << hb) / sc;
       bucket0 = (w << bb) + ((g * len) << lb) + l;
       stride = 1u << lb;
       dst = outD + (size_t)jj * XW;
     }
   }
-  const uint32_t L = (len + 63) >> 6;  // strip per lane
-  const uint32_t Lr = (((1u << lb) / sr) + 63) >> 6, Lc = (((1u << hb) / sc) + 63) >> 6;
+  const uint32_t L = (len + m - 1) / m;  // strip per lane
+  const uint32_t Lr = (((1u << lb) / sr) + 63) >> 6, Lc = (((1u << hb) / sc) + mc - 1) / mc;
   const uint32_t Lmax = Lr > Lc ? Lr : Lc;  // block-uniform loop bound
   Xyzz<F> v = xyzz_inf<F>();
   for (uint32_t step = 0; step < Lmax + 6; step++) {
     Xyzz<F> q;
     bool act = false;
     if (step < Lmax) {
-      const uint32_t t = lane * L + step;
+      const uint32_t t = sub * L + step;
       if (live && step < L && t < len) {
         const uint32_t b = bucket0 + t * stride;
         if (bstart[b + 1] > bstart[b]) {
@@ -1314,19 +1325,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
           act = true;
         }
       }
-    } else {
+    } else {  // tree levels 32 .. 1 (block-uniform barriers; levels >= m idle)
       const uint32_t sz = 32u >> (step - Lmax);
-      if (lane >= sz && lane < 2 * sz) sh[wave][lane - sz] = v;
+      if (sz < m && sub >= sz && sub < 2 * sz) sh[wave][lslot + sub - sz] = v;
       __syncthreads();
-      if (lane < sz) {
-        q = sh[wave][lane];
+      if (sz < m && sub < sz) {
+        q = sh[wave][lslot + sub];
         act = !xyzz_is_inf(q);
       }
     }
     if (act) v = xyzz_is_inf(v) ? q : br_add<G>(v, q);
     if (step >= Lmax) __syncthreads();
   }
-  if (live && lane == 0) st_xyzz<G>(dst, v);
+  if (live && sub == 0) st_xyzz<G>(dst, v);
 }
 
 // Row / column sums in two kernels that keep every issued addition useful
@@ -2261,6 +2272,7 @@ struct BrGeom {
   int mode;
   int S;  // mode 2: buckets per lane in k_br_fold
   int sr, sc, sb, segt;
+  int mc = 64;  // mode 1: lanes per column segment (k_msm_br_strip)
 };
 static BrGeom br_geom(const MsmPlan& P, bool g2) {
   static const int env_mode = [] {
@@ -2269,7 +2281,7 @@ static BrGeom br_geom(const MsmPlan& P, bool g2) {
   }();
   static const int strip_fold = [] {  // mode 1: buckets folded per lane before the tree
     const char* e = getenv("ZKMI_BR_STRIP");
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 8;  // 16 (+ two 512-bucket columns per wave) measured slower: 2^20 1 lane 0.38 -> 0.46 ms
   }();
   static const int strip_fold2 = [] {  // mode 1, G2 (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
     const char* e = getenv("ZKMI_BR_STRIP_G2");
@@ -2298,6 +2310,10 @@ static BrGeom br_geom(const MsmPlan& P, bool g2) {
     const int segb = g.mode == 1 ? 64 * fold : 256;  // buckets per wave job
     g.sr = (1 << P.lb) > segb ? (1 << P.lb) / segb : 1;
     g.sc = (1 << P.hb) > segb ? (1 << P.hb) / segb : 1;
+    // lanes per column segment: as many as keep `fold` buckets per lane
+    const int lenc = (1 << P.hb) / g.sc;
+    g.mc = 64;
+    while (g.mc > 1 && lenc / g.mc < fold) g.mc >>= 1;
   }
   const uint32_t maxterms = std::max((1u << P.hb) * g.sr, (1u << (P.lb - 1)) * g.sc);
   g.sb = (int)((maxterms + g.segt - 1) / g.segt);
@@ -2468,9 +2484,11 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       auto wgs = [](uint32_t lines, uint32_t len) { return len >= 256 ? lines : lines / (256 / len); };
       const uint32_t nwr = wgs((uint32_t)W << hb, (1u << lb) / bg.S), nwc = wgs((uint32_t)W << lb, (1u << hb) / bg.S);
       k_br_lines<G><<<nwr + nwc, 256, 256 * XW * 4, brs>>>(part, lb, hb, W, bg.S, nwr, Cb, Db);
-    } else if (bg.mode == 1) {  // one wave per row / column
-      uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc));
-      k_msm_br_strip<G><<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, bstart, lb, hb, W, sr, sc, Cb, Db);
+    } else if (bg.mode == 1) {  // one wave per row segment, 64 / mc column segments per wave
+      const uint32_t nrow = (uint32_t)W * ((1u << hb) * sr), ncol = (uint32_t)W * ((1u << lb) * sc);
+      const uint32_t cpw = 64u / (uint32_t)bg.mc;
+      const uint32_t jobs1 = nrow + (ncol + cpw - 1) / cpw;
+      k_msm_br_strip<G><<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, bstart, lb, hb, W, sr, sc, bg.mc, Cb, Db);
     } else {
       uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc));
       k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, 256, Cb, Db);
