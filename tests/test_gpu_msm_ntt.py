@@ -338,6 +338,20 @@ def test_bucket_reduction_mode2_subprocess():
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
 
 
+def test_negated_table_subprocess():
+    """The opt-in negated fixed-base table (ZKMI_NEG_TABLE=1: -P rows gathered
+    for negative digits on the one-lane-per-bucket path) equals the oracle for
+    the same tables as the fold + lines check (G1 c = 19, 20, 22; G2 c = 20,
+    with an infinity base)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, ZKMI_NEG_TABLE="1")
+    r = subprocess.run([sys.executable, "-c", _BR_MODE2_SCRIPT, os.path.dirname(here), here], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_bases_arith_stream_matches_oracle(ctx):
     """zkmi_bases_generate_arith_g1 (P_i = P0 + (first + i) D in HBM, the
     bench's §8d point stream) equals the oracle's P0 + i D points."""

@@ -961,6 +961,7 @@ __global__ void __launch_bounds__(256) k_items_scatter(const uint32_t* __restric
 template <class G>
 __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
                                                const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
+                                               const uint32_t* __restrict__ nbases,
                                                uint32_t tn, uint32_t tskip, uint32_t* __restrict__ buckets,
                                                uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                                                uint32_t* __restrict__ xpts) {
@@ -974,7 +975,8 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
   auto row = [&](uint32_t v) {
     uint32_t idx = v & 0x7FFFFFFFu;
     if (tskip) idx += (idx / tn) * tskip;
-    return reinterpret_cast<const uint4*>(bases + (size_t)idx * G::PW);
+    const uint32_t* src = nbases && (v >> 31) ? nbases : bases;  // -P rows for a negative digit
+    return reinterpret_cast<const uint4*>(src + (size_t)idx * G::PW);
   };
   constexpr bool PF = G::CW == 8;  // G2: see msm_acc0_body
   Xyzz<F> acc = xyzz_inf<F>();
@@ -1008,12 +1010,15 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
     const uint32_t* w = reinterpret_cast<const uint32_t*>(cr);
     if (w[G::PW - 1] >> 31) continue;  // base at infinity
     Aff<F> P;
+    const bool ng = !nbases && (v >> 31);  // sign still to apply (no negated table)
     if constexpr (G::CW == 8) {
       P.x = unpack(w);
-      P.y = fq_cneg(unpack(w + 8), v >> 31);
+      P.y = unpack(w + 8);
+      if (ng) P.y = fq_cneg(P.y, true);
     } else {
       P.x = {unpack(w), unpack(w + 8)};
-      P.y = {fq_cneg(unpack(w + 16), v >> 31), fq_cneg(unpack(w + 24), v >> 31)};
+      P.y = {unpack(w + 16), unpack(w + 24)};
+      if (ng) P.y = {fq_cneg(P.y.c0, true), fq_cneg(P.y.c1, true)};
     }
     acc_step<G>(acc, naff, P);
   }
@@ -1027,17 +1032,19 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
 }
 __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
     k_acc_items_g1(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
-                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
+                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
+                   const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                    uint32_t* __restrict__ xpts) {
-  acc_items_body<G1T>(items, nitems, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts);
+  acc_items_body<G1T>(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts);
 }
 __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
     k_acc_items_g2(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
-                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
+                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
+                   const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                    uint32_t* __restrict__ xpts) {
-  acc_items_body<G2T>(items, nitems, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts);
+  acc_items_body<G2T>(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts);
 }
 
 // Buckets split into 2..ITEM_SEQ_MAX pieces: one thread sums them (contiguous
@@ -1909,6 +1916,29 @@ int bases_upload(zkmi_ctx* ctx, int g2, const uint64_t* host_affine, size_t n, z
   return bases_from_device_canon(ctx, g2, d_tmp, n, out);
 }
 
+// neg[r] = (x, 2p - y) for every table row r (both Fq2 components for G2) --
+// exactly the y that fq_cneg produces -- infinity rows copied as they are
+template <class G>
+__global__ void __launch_bounds__(256) k_bases_negate(const uint32_t* __restrict__ in, size_t rows,
+                                                      uint32_t* __restrict__ out) {
+  const size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const uint32_t* p = in + r * G::PW;
+  uint32_t* q = out + r * G::PW;
+  uint32_t w[G::PW];
+#pragma unroll
+  for (int k = 0; k < G::PW; k++) w[k] = p[k];
+  if (!(w[G::PW - 1] >> 31)) {
+#pragma unroll
+    for (int c = G::PW / 2; c < G::PW; c += 8) {  // the y components
+      const Fe y = fq_cneg(unpack(w + c), true);
+      pack(w + c, y);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < G::PW; k++) q[k] = w[k];
+}
+
 int bases_precompute(zkmi_bases* b, int c, int factor) {
   if (c < 4 || c > 22) {
     set_error("bases_precompute: window %d outside [4, 22]", c);
@@ -1960,6 +1990,32 @@ int bases_precompute(zkmi_bases* b, int c, int factor) {
   b->tc = c;
   b->tp = p;
   b->tw = Wp;
+  // negated copy for the one-lane-per-bucket path (2^(c-1) >= ITEMS_MIN_K),
+  // only while HBM stays comfortably free (MSM workspaces come later)
+  // Opt-in (ZKMI_NEG_TABLE=1): the gathers then spread over twice the table,
+  // which cancels the ~60 instructions per entry it saves (tools/neg_ab2.sh:
+  // 2^20 3-lane 830-836 Mpt/s either way, 2^26 984 with vs 997 without), and
+  // it doubles the table's HBM.
+  static const bool use_neg = [] {
+    const char* e = getenv("ZKMI_NEG_TABLE");
+    return e && atoi(e) != 0;
+  }();
+  if (use_neg && (1u << (c - 1)) >= ITEMS_MIN_K && b->n) {
+    size_t fr = 0, tot = 0;
+    const size_t bytes = row * p;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 2 * bytes + ((size_t)16 << 30)) {
+      uint32_t* d_neg = nullptr;
+      if (hipMalloc(&d_neg, bytes) == hipSuccess) {
+        const size_t rows = b->n * (size_t)p;
+        const unsigned grid = (unsigned)((rows + 255) / 256);
+        if (b->g2) k_bases_negate<G2T><<<grid, 256, 0, st>>>(d_tab, rows, d_neg);
+        else k_bases_negate<G1T><<<grid, 256, 0, st>>>(d_tab, rows, d_neg);
+        if (hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess) b->d_neg = d_neg;
+        else hipFree(d_neg);
+      }
+      (void)hipGetLastError();
+    }
+  }
   return 0;
 }
 
@@ -2402,7 +2458,9 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     {
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
       auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
-      kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, tn, tskip, buckets,
+      const uint32_t* d_nbases = tb->d_neg ? tb->d_neg + offset * G::PW : nullptr;
+      kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, d_nbases, tn, tskip,
+                                                               buckets,
                                                                xkey, xvalid, xpts);
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);

@@ -232,6 +232,7 @@ void zkmi_bases_destroy(zkmi_bases* b) {
   ZK_DEVICE_GUARD(b);
   if (!b) return;
   hipFree(b->d_pts);
+  if (b->d_neg) hipFree(b->d_neg);
   delete b;
 }
 size_t zkmi_bases_len(const zkmi_bases* b) { return b ? b->n : 0; }

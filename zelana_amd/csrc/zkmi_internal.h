@@ -84,6 +84,10 @@ struct zkmi_bases {
   int tc = 0;  // table window (0 = no table: plain bases, any window)
   int tp = 1;  // copies
   int tw = 0;  // windows per copy
+  // The table again with every y negated (same layout), so the one-lane-per-
+  // bucket accumulation gathers -P for a negative digit instead of negating
+  // per entry; opt-in (ZKMI_NEG_TABLE=1, measured level), null otherwise.
+  uint32_t* d_neg = nullptr;
 };
 
 // Multi-rank communicator (zkmi.h multi-GPU section; comm.hip).
