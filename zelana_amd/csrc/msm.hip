@@ -137,24 +137,45 @@ __device__ __forceinline__ Xyzz<typename G::F> br_add(const Xyzz<typename G::F>&
 // ----------------------------------------------------------------- digits
 __host__ __device__ constexpr int msm_windows(int c) { return (254 + c - 1) / c + ((254 % c) == 0 ? 1 : 0); }
 
-template <int C>
+// Window layout of a scalar: W(C) windows.  Uniform (BAL = false): window w
+// covers bits [wC, wC + C), the top one only what is left of 254 bits, so its
+// digits reach 2^(254 - (W-1)C) buckets at most -- with a full fixed-base
+// table that short top window piles a whole copy's n entries onto those few
+// buckets (2^20 at c = 20: 2^13 buckets of ~150 entries, split and re-summed
+// after the accumulation).  Balanced (BAL, full tables only): the first A
+// windows are C bits wide and the rest C - 1, A = 254 - W (C - 1), so every
+// copy spreads over 2^(C-2) or 2^(C-1) buckets; the top window (C - 1 bits
+// plus the carry) still fits the 2^(C-1) buckets.  (When W (C - 1) >= 254,
+// A = 0: every window C - 1 bits, the top one what is left.)  Copy j of the
+// table is 2^(offset of window j) P_i (bases_precompute).
+template <int C, bool BAL>
+struct WinLayout {
+  static constexpr int W = msm_windows(C);
+  static constexpr int A = BAL ? (254 - W * (C - 1) > 0 ? 254 - W * (C - 1) : 0) : W;  // windows of width C
+  static_assert(A >= 0 && A <= W && (!BAL || A < W), "balanced layout");
+  static constexpr int width(int w) { return w < A ? C : C - 1; }
+  static constexpr int offset(int w) { return w <= A ? w * C : A * C + (w - A) * (C - 1); }
+};
+
+template <int C, bool BAL = false>
 __device__ __forceinline__ void scalar_digits(const uint32_t* __restrict__ scalars, size_t i, int32_t* d) {
   uint4 a = reinterpret_cast<const uint4*>(scalars)[2 * i];
   uint4 b = reinterpret_cast<const uint4*>(scalars)[2 * i + 1];
   // mask to 254 bits: keeps every digit inside its window's bucket range even
   // for a non-canonical input (documented: scalars must be < r)
   uint32_t s[9] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w & 0x3FFFFFFFu, 0};
-  constexpr int W = msm_windows(C);
-  constexpr uint32_t HALF = 1u << (C - 1);
+  using L = WinLayout<C, BAL>;
+  constexpr int W = L::W;
   uint32_t carry = 0;
 #pragma unroll
   for (int w = 0; w < W; w++) {
-    const int bit = w * C, wi = bit >> 5, sh = bit & 31;
+      const int bit = L::offset(w), wi = bit >> 5, sh = bit & 31, wd = L::width(w);
+    const uint32_t half = 1u << (wd - 1);
     uint64_t v64 = (((uint64_t)s[wi + 1 < 9 ? wi + 1 : 8]) << 32) | s[wi < 9 ? wi : 8];
-    uint32_t v = (uint32_t)(v64 >> sh) & ((1u << C) - 1);
+    uint32_t v = (uint32_t)(v64 >> sh) & ((1u << wd) - 1);
     v += carry;
-    if (w < W - 1 && v > HALF) {
-      d[w] = (int32_t)v - (int32_t)(1u << C);
+    if (w < W - 1 && v > half) {
+      d[w] = (int32_t)v - (int32_t)(1u << wd);
       carry = 1;
     } else {
       d[w] = (int32_t)v;
@@ -169,14 +190,14 @@ __device__ __forceinline__ void scalar_digits(const uint32_t* __restrict__ scala
 // (p = 1, Wp = W without a table).  Digits depend on the scalars only (bases
 // at infinity are skipped in the accumulation), so MSMs with the same
 // scalars over different base sets share one sort (msm_submit_shared).
-template <int C>
+template <int C, bool BAL>
 __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars, size_t n, int p, int Wp,
                                                     int32_t* __restrict__ digits) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   constexpr int W = msm_windows(C);
   int32_t d[W];
-  scalar_digits<C>(scalars, i, d);
+  scalar_digits<C, BAL>(scalars, i, d);
 #pragma unroll
   for (int w = 0; w < W; w++) {
     int j = w / Wp, wq = w - j * Wp;
@@ -380,12 +401,12 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_scatter(const int32_t* __r
 // digit layout of k_msm_digits (key w' * B + |d| - 1, value (j * n + i) | sign);
 // a P1 chunk is CS scalars.  No digits array: its write and two reads go
 // (2^26 table MSM: 3.2 GB written + 6.4 GB read).
-template <int C>
+template <int C, bool BAL>
 __device__ __forceinline__ void rs_scalar_keys(const uint32_t* __restrict__ scalars, size_t i, size_t n, int Wp,
                                                uint32_t B, uint32_t* key, uint32_t* val, bool* ok) {
   constexpr int W = msm_windows(C);
   int32_t d[W];
-  scalar_digits<C>(scalars, i, d);
+  scalar_digits<C, BAL>(scalars, i, d);
   uint32_t j = 0, wq = 0;
 #pragma unroll
   for (int w = 0; w < W; w++) {
@@ -400,7 +421,7 @@ __device__ __forceinline__ void rs_scalar_keys(const uint32_t* __restrict__ scal
   }
 }
 
-template <int C>
+template <int C, bool BAL>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_count(const uint32_t* __restrict__ scalars, size_t n, int Wp,
                                                              uint32_t B, uint32_t NH, uint32_t lob, uint32_t CS,
                                                              uint32_t nc1, uint32_t* __restrict__ cnt1) {
@@ -412,7 +433,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_count(const uint32_t* __r
   for (uint32_t k = threadIdx.x; k < CS && base + k < n; k += RS_THREADS) {
     uint32_t key[W], val[W];
     bool ok[W];
-    rs_scalar_keys<C>(scalars, base + k, n, Wp, B, key, val, ok);
+    rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok);
 #pragma unroll
     for (int w = 0; w < W; w++)
       if (ok[w]) atomicAdd(&hist[key[w] >> lob], 1u);
@@ -423,7 +444,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_count(const uint32_t* __r
 
 // T threads: a sub-tile is T scalars (T * W entries); 1024 gives 4x longer
 // runs per bin than 256 (one workgroup per CU, 16 waves)
-template <int C, int T>
+template <int C, int T, bool BAL>
 __global__ void __launch_bounds__(T) k_rs_p1f_scatter(const uint32_t* __restrict__ scalars, size_t n, int Wp,
                                                                uint32_t B, uint32_t NH, uint32_t lob, uint32_t CS,
                                                                uint32_t nc1, const uint32_t* __restrict__ offs1,
@@ -436,7 +457,7 @@ __global__ void __launch_bounds__(T) k_rs_p1f_scatter(const uint32_t* __restrict
   auto fill = [&](uint32_t sub, uint32_t* key, uint32_t* val, bool* ok) {
     const uint32_t k = sub * T + threadIdx.x;
     if (k < cnt) {
-      rs_scalar_keys<C>(scalars, base + k, n, Wp, B, key, val, ok);
+      rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok);
     } else {
 #pragma unroll
       for (int w = 0; w < W; w++) ok[w] = false;
@@ -884,23 +905,33 @@ constexpr uint32_t ITEMS_MIN_K = 1u << 18;
 constexpr uint32_t ITEM_SEQ_MAX = 32;  // pieces summed by one thread (k_items_combine)
 constexpr uint32_t NOSLOT = 0xFFFFFFFFu;
 
+// ITEMS_IPT buckets per thread (strided by 256): a workgroup then covers 2K
+// buckets, so the per-class global atomics at its end (bucket sizes of a
+// uniform MSM fall into ~20 classes) see 256 workgroups for 2^19 buckets
+// rather than 2048 -- same-address atomics serialise in L2.
+constexpr uint32_t ITEMS_IPT = 8;
 __global__ void __launch_bounds__(256) k_items_count(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
                                                      uint32_t* __restrict__ hist, uint32_t* __restrict__ hv,
                                                      uint32_t* __restrict__ open_flag) {
   __shared__ uint32_t lh[ITEM_CAP_MAX + 1];
   for (uint32_t i = threadIdx.x; i <= cap; i += 256) lh[i] = 0;
   __syncthreads();
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b < K) {
-    const uint32_t size = bstart[b + 1] - bstart[b];
-    const uint32_t np = (size + cap - 1) / cap;
-    if (size) {
-      if (np > 1) atomicAdd(&lh[cap], np - 1);
-      atomicAdd(&lh[size - (np - 1) * cap], 1u);
+  bool open = false;
+#pragma unroll
+  for (uint32_t q = 0; q < ITEMS_IPT; q++) {
+    const uint32_t b = (blockIdx.x * ITEMS_IPT + q) * 256 + threadIdx.x;
+    if (b < K) {
+      const uint32_t size = bstart[b + 1] - bstart[b];
+      const uint32_t np = (size + cap - 1) / cap;
+      if (size) {
+        if (np > 1) atomicAdd(&lh[cap], np - 1);
+        atomicAdd(&lh[size - (np - 1) * cap], 1u);
+      }
+      hv[b] = np > 1 ? np : 0;
+      open |= np > ITEM_SEQ_MAX;
     }
-    hv[b] = np > 1 ? np : 0;
-    if (np > ITEM_SEQ_MAX) atomicOr(open_flag, 1u);
   }
+  if (open) atomicOr(open_flag, 1u);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i <= cap; i += 256)
     if (lh[i]) atomicAdd(&hist[i], lh[i]);
@@ -934,27 +965,34 @@ __global__ void __launch_bounds__(256) k_items_scatter(const uint32_t* __restric
   __shared__ uint32_t lc[ITEM_CAP_MAX + 1], lbase[ITEM_CAP_MAX + 1];
   for (uint32_t i = threadIdx.x; i <= cap; i += 256) lc[i] = 0;
   __syncthreads();
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  uint32_t lo = 0, size = 0, np = 0, r_full = 0, r_last = 0, cl_last = 0;
-  if (b < K) {
-    lo = bstart[b];
-    size = bstart[b + 1] - lo;
-    np = (size + cap - 1) / cap;
-    if (size) {
-      if (np > 1) r_full = atomicAdd(&lc[cap], np - 1);
-      cl_last = size - (np - 1) * cap;
-      r_last = atomicAdd(&lc[cl_last], 1u);
+  uint32_t r_full[ITEMS_IPT], r_last[ITEMS_IPT];
+#pragma unroll
+  for (uint32_t q = 0; q < ITEMS_IPT; q++) {
+    const uint32_t b = (blockIdx.x * ITEMS_IPT + q) * 256 + threadIdx.x;
+    r_full[q] = r_last[q] = 0;
+    if (b < K) {
+      const uint32_t size = bstart[b + 1] - bstart[b];
+      const uint32_t np = (size + cap - 1) / cap;
+      if (size) {
+        if (np > 1) r_full[q] = atomicAdd(&lc[cap], np - 1);
+        r_last[q] = atomicAdd(&lc[size - (np - 1) * cap], 1u);
+      }
     }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i <= cap; i += 256) lbase[i] = lc[i] ? atomicAdd(&cursor[i], lc[i]) : 0;
   __syncthreads();
-  if (b < K && size) {
+#pragma unroll
+  for (uint32_t q = 0; q < ITEMS_IPT; q++) {
+    const uint32_t b = (blockIdx.x * ITEMS_IPT + q) * 256 + threadIdx.x;
+    if (b >= K) continue;
+    const uint32_t lo = bstart[b], size = bstart[b + 1] - lo;
+    if (!size) continue;
+    const uint32_t np = (size + cap - 1) / cap, cl_last = size - (np - 1) * cap;
     const uint32_t pb = np > 1 ? pbase[b] : NOSLOT;
-    for (uint32_t q = 0; q + 1 < np; q++)
-      items[lbase[cap] + r_full + q] = make_uint4(lo + q * cap, lo + (q + 1) * cap, b, pb + q);
-    items[lbase[cl_last] + r_last] =
-        make_uint4(lo + (np - 1) * cap, lo + size, b, np > 1 ? pb + (np - 1) : NOSLOT);
+    for (uint32_t k = 0; k + 1 < np; k++)
+      items[lbase[cap] + r_full[q] + k] = make_uint4(lo + k * cap, lo + (k + 1) * cap, b, pb + k);
+    items[lbase[cl_last] + r_last[q]] = make_uint4(lo + (np - 1) * cap, lo + size, b, np > 1 ? pb + (np - 1) : NOSLOT);
   }
 }
 
@@ -1646,8 +1684,10 @@ __device__ __forceinline__ Fe2 inv_any<Fq2Ops>(const Fe2& a) {
   Fe ni = fq_inv(nrm);
   return Fe2{mul<FqP>(a.c0, ni), neg<FqP>(mul<FqP>(a.c1, ni))};
 }
+// Copy j >= 1 is copy j-1 doubled `shift` times, or shift - 1 times once
+// j - 1 >= wide (balanced window widths, WinLayout; wide = p: uniform).
 template <class G>
-__global__ void __launch_bounds__(256) k_bases_table(uint32_t* __restrict__ pts, size_t n, int shift, int p,
+__global__ void __launch_bounds__(256) k_bases_table(uint32_t* __restrict__ pts, size_t n, int shift, int wide, int p,
                                                      uint32_t* __restrict__ bad) {
   using F = typename G::F;
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -1662,7 +1702,8 @@ __global__ void __launch_bounds__(256) k_bases_table(uint32_t* __restrict__ pts,
       continue;
     }
     Xyzz<F> acc = xyzz_mdbl(q);
-    for (int k = 1; k < shift; k++) acc = xyzz_dbl(acc);
+    const int dbls = j - 1 < wide ? shift : shift - 1;
+    for (int k = 1; k < dbls; k++) acc = xyzz_dbl(acc);
     if (xyzz_is_inf(acc)) {  // impossible without 2-power torsion; refuse
       atomicOr(bad, 1u);
       return;
@@ -1971,10 +2012,19 @@ int bases_precompute(zkmi_bases* b, int c, int factor) {
   uint32_t bad = 0;
   hipError_t e = hipMemsetAsync(d_bad, 0, 4, st);
   if (e == hipSuccess && b->n) e = hipMemcpyAsync(d_tab, b->d_pts, b->n * pw * 4, hipMemcpyDeviceToDevice, st);
+  // full tables (one window per copy) use the balanced widths (WinLayout):
+  // no short top window piling a copy's entries onto a few buckets.
+  // ZKMI_TABLE_BAL=0 keeps the uniform layout (A/B only).
+  static const bool bal_env = [] {
+    const char* e = getenv("ZKMI_TABLE_BAL");
+    return !e || atoi(e) != 0;
+  }();
+  const bool bal = bal_env && Wp == 1 && c >= 4;
+  const int wide = bal ? std::max(0, 254 - W * (c - 1)) : p;
   if (e == hipSuccess && b->n && p > 1) {
     unsigned grid = (unsigned)((b->n + 255) / 256);
-    if (b->g2) k_bases_table<G2T><<<grid, 256, 0, st>>>(d_tab, b->n, c * Wp, p, d_bad);
-    else k_bases_table<G1T><<<grid, 256, 0, st>>>(d_tab, b->n, c * Wp, p, d_bad);
+    if (b->g2) k_bases_table<G2T><<<grid, 256, 0, st>>>(d_tab, b->n, c * Wp, wide, p, d_bad);
+    else k_bases_table<G1T><<<grid, 256, 0, st>>>(d_tab, b->n, c * Wp, wide, p, d_bad);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st);
@@ -1990,6 +2040,7 @@ int bases_precompute(zkmi_bases* b, int c, int factor) {
   b->tc = c;
   b->tp = p;
   b->tw = Wp;
+  b->tbal = bal ? 1 : 0;
   // negated copy for the one-lane-per-bucket path (2^(c-1) >= ITEMS_MIN_K),
   // only while HBM stays comfortably free (MSM workspaces come later)
   // Opt-in (ZKMI_NEG_TABLE=1): the gathers then spread over twice the table,
@@ -2059,13 +2110,15 @@ static int pick_window(size_t n) {
 }
 
 template <int C>
-static void launch_digits(hipStream_t st, const uint32_t* sc, size_t n, int p, int Wp, int32_t* dg) {
-  k_msm_digits<C><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(sc, n, p, Wp, dg);
+static void launch_digits(hipStream_t st, const uint32_t* sc, size_t n, int p, int Wp, bool bal, int32_t* dg) {
+  if (bal) k_msm_digits<C, true><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(sc, n, p, Wp, dg);
+  else k_msm_digits<C, false><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(sc, n, p, Wp, dg);
 }
-static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, size_t n, int p, int Wp, int32_t* dg) {
+static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, size_t n, int p, int Wp, bool bal,
+                           int32_t* dg) {
   switch (c) {
 #define ZK_C(CC) \
-  case CC: launch_digits<CC>(st, sc, n, p, Wp, dg); break;
+  case CC: launch_digits<CC>(st, sc, n, p, Wp, bal, dg); break;
     ZK_C(4) ZK_C(5) ZK_C(6) ZK_C(7) ZK_C(8) ZK_C(9) ZK_C(10) ZK_C(11) ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15)
     ZK_C(16) ZK_C(17) ZK_C(18) ZK_C(19) ZK_C(20) ZK_C(21) ZK_C(22)
 #undef ZK_C
@@ -2076,7 +2129,7 @@ static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, size_t n, 
   return 0;
 }
 
-template <int C>
+template <int C, bool BAL>
 static void launch_p1_fused(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t NH,
                             uint32_t lob, uint32_t CS, uint32_t nf, uint32_t* cnt1, uint32_t* okey, uint32_t* oval,
                             bool scatter) {
@@ -2089,19 +2142,23 @@ static void launch_p1_fused(hipStream_t st, const uint32_t* sc, size_t n, int Wp
   }();
   constexpr int W = msm_windows(C);
   if (scatter && env_t1 == 1024 && rs_scatter_lds(NH, 1024 * W, 1024) <= 160 * 1024)
-    k_rs_p1f_scatter<C, 1024><<<nf, 1024, rs_scatter_lds(NH, 1024 * W, 1024), st>>>(sc, n, Wp, B, NH, lob, CS, nf,
+    k_rs_p1f_scatter<C, 1024, BAL><<<nf, 1024, rs_scatter_lds(NH, 1024 * W, 1024), st>>>(sc, n, Wp, B, NH, lob, CS, nf,
                                                                                     cnt1, okey, oval);
   else if (scatter)
-    k_rs_p1f_scatter<C, RS_THREADS><<<nf, RS_THREADS, rs_scatter_lds(NH, RS_THREADS * W), st>>>(
+    k_rs_p1f_scatter<C, RS_THREADS, BAL><<<nf, RS_THREADS, rs_scatter_lds(NH, RS_THREADS * W), st>>>(
         sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval);
   else
-    k_rs_p1f_count<C><<<nf, RS_THREADS, NH * 4, st>>>(sc, n, Wp, B, NH, lob, CS, nf, cnt1);
+    k_rs_p1f_count<C, BAL><<<nf, RS_THREADS, NH * 4, st>>>(sc, n, Wp, B, NH, lob, CS, nf, cnt1);
 }
-static int p1_fused(int c, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t NH, uint32_t lob,
-                    uint32_t CS, uint32_t nf, uint32_t* cnt1, uint32_t* okey, uint32_t* oval, bool scatter) {
+static int p1_fused(int c, bool bal, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t NH,
+                    uint32_t lob, uint32_t CS, uint32_t nf, uint32_t* cnt1, uint32_t* okey, uint32_t* oval,
+                    bool scatter) {
   switch (c) {
-#define ZK_C(CC) \
-  case CC: launch_p1_fused<CC>(st, sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval, scatter); break;
+#define ZK_C(CC)                                                                                  \
+  case CC:                                                                                        \
+    if (bal) launch_p1_fused<CC, true>(st, sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval, scatter); \
+    else launch_p1_fused<CC, false>(st, sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval, scatter);    \
+    break;
     ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15) ZK_C(16) ZK_C(17) ZK_C(18) ZK_C(19) ZK_C(20) ZK_C(21) ZK_C(22)
 #undef ZK_C
     default:
@@ -2153,6 +2210,7 @@ static int get_lane(zkmi_ctx* ctx, MsmLane** out) {
 // Window / table plan of one MSM over base set tb.
 struct MsmPlan {
   int c, p, W, bb, lb, hb;
+  bool bal;  // balanced window widths (full tables built with them, WinLayout)
   size_t ne, Mmax;
   uint32_t B, K;
 };
@@ -2163,6 +2221,7 @@ static MsmPlan msm_plan(const zkmi_ctx* ctx, const zkmi_bases* tb, size_t n) {
   P.c = table ? tb->tc : (ctx->msm_window > 0 ? ctx->msm_window : pick_window(n));
   P.p = table ? tb->tp : 1;
   P.W = table ? tb->tw : msm_windows(P.c);  // windows actually run
+  P.bal = table && tb->tbal;
   P.ne = (size_t)P.p * n;                   // entries per window
   P.Mmax = (size_t)P.W * P.ne;
   P.B = 1u << (P.c - 1);
@@ -2172,7 +2231,9 @@ static MsmPlan msm_plan(const zkmi_ctx* ctx, const zkmi_bases* tb, size_t n) {
   P.hb = P.bb - P.lb;
   return P;
 }
-static bool same_plan(const MsmPlan& a, const MsmPlan& b) { return a.c == b.c && a.p == b.p && a.W == b.W; }
+static bool same_plan(const MsmPlan& a, const MsmPlan& b) {
+  return a.c == b.c && a.p == b.p && a.W == b.W && a.bal == b.bal;
+}
 
 // exclusive scan of a[0..len) in place; *total = sum (bsums: len/1024 + 1 words)
 static void scan_excl(hipStream_t st, uint32_t* a, size_t len, uint32_t* bsums, uint32_t* total) {
@@ -2248,7 +2309,7 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   lane->debug_sorted = 1;
   ScopedKernelTimer tm(ctx, "msm_sort", st);
   if (!fused) {
-    ZK_TRY(dispatch_digits(P.c, st, d_scalars, n, P.p, P.W, digits));
+    ZK_TRY(dispatch_digits(P.c, st, d_scalars, n, P.p, P.W, P.bal, digits));
     ZK_HIP(hipEventRecord(lane->consumed, st));
     ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
   }
@@ -2265,9 +2326,9 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   const int st2 = env_st2 ? env_st2 : 8192;
   const uint32_t ne = (uint32_t)P.ne;
   if (fused) {
-    ZK_TRY(p1_fused(P.c, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, nullptr, nullptr, false));
+    ZK_TRY(p1_fused(P.c, P.bal, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, nullptr, nullptr, false));
     scan(cnt1, (size_t)NH * nf, &tot[0]);
-    ZK_TRY(p1_fused(P.c, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, okey, oval, true));
+    ZK_TRY(p1_fused(P.c, P.bal, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, okey, oval, true));
     ZK_HIP(hipEventRecord(lane->consumed, st));
     ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
   } else {
@@ -2449,11 +2510,11 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       lane->debug_sorted = 2;
       ScopedKernelTimer tm(ctx, "msm_items_plan", st);
       ZK_HIP(hipMemsetAsync(hist, 0, (ITEM_CAP_MAX + 1) * 4, st));
-      k_items_count<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hist, hv, &flags[0]);
+      const unsigned ig = (K + 256 * ITEMS_IPT - 1) / (256 * ITEMS_IPT);
+      k_items_count<<<ig, 256, 0, st>>>(bstart, K, cap, hist, hv, &flags[0]);
       scan_excl(st, hv, K, bsums, &nitems[1]);
       k_items_offsets<<<1, 1, 0, st>>>(hist, cap, cursor, &nitems[0]);
-      k_items_scatter<<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, cursor, items, &flags[0], xkey, xvalid,
-                                                       (uint32_t)xl);
+      k_items_scatter<<<ig, 256, 0, st>>>(bstart, K, cap, hv, cursor, items, &flags[0], xkey, xvalid, (uint32_t)xl);
     }
     {
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);

@@ -79,11 +79,14 @@ struct zkmi_bases {
   size_t n;
   uint32_t* d_pts;  // packed affine, internal Montgomery, inf flag = bit 31 of last word
   // Fixed-base table (zkmi_bases_precompute): d_pts holds tp copies of the n
-  // points, copy j = 2^(tc * tw * j) * P_i, so an MSM with window tc runs tw
+  // points, copy j = 2^(tc * tw * j) * P_i (tbal: see below), so an MSM with window tc runs tw
   // windows of tp*n entries instead of tp*tw windows of n entries.
   int tc = 0;  // table window (0 = no table: plain bases, any window)
   int tp = 1;  // copies
   int tw = 0;  // windows per copy
+  // 1: full table (tw = 1) with balanced window widths -- copy j is
+  // 2^(offset of window j) * P_i, WinLayout<tc, true> in msm.hip
+  int tbal = 0;
   // The table again with every y negated (same layout), so the one-lane-per-
   // bucket accumulation gathers -P for a negative digit instead of negating
   // per entry; opt-in (ZKMI_NEG_TABLE=1, measured level), null otherwise.
