@@ -218,7 +218,24 @@ int main() {
   }
   int checks = 0;
   for (int trial = 0; trial < 200; trial++) {
-    Xyzz<F> a = xyzz_inf<F>(), b = xyzz_inf<F>(), c = xyzz_inf<F>();
+    Xyzz<F> a = xyzz_inf<F>(), b = xyzz_inf<F>(), c = xyzz_inf<F>(), df = xyzz_inf<F>();
+    int dphase = 0;  // acc_items_g1 rule: 0 empty, 1 one affine point, 2 xyzz_madd_g1f
+    // y of a base as the one-lane-per-bucket G1 kernel feeds it: borrow-form 2p - y
+    // (limb-wise, unnormalised) for a negative digit
+    auto dstep = [&](const Aff<F>& q, bool ng) {
+      const Fe y = ng ? bsub(FqP::B2_1, q.y) : q.y;
+      if (dphase == 0) {
+        df = xyzz_from_aff(Aff<F>{q.x, reduce_q32<FqP>(y)});
+        dphase = 1;
+      } else if (dphase == 1) {
+        df = xyzz_mmadd_g1({df.x, df.y}, Aff<F>{q.x, reduce_q32<FqP>(y)});
+        dphase = xyzz_is_inf(df) ? 0 : 2;
+      } else {
+        bool inf = false;
+        df = xyzz_madd_g1f(df, q.x, y, &inf);
+        if (inf) dphase = 0;
+      }
+    };
     bool naff = false;  // msm.hip acc_step: first point as is, second by xyzz_mmadd_g1
     auto step = [&](const Aff<F>& q) {
       if (xyzz_is_inf(c)) {
@@ -246,6 +263,7 @@ int main() {
       a = xyzz_madd(a, qa);
       b = xyzz_madd_g1(b, qb);
       step(qb);
+      dstep(q, neg_);
       if (mode == 1) {  // cancel: add -Q right after Q
         Aff<F> na = qa, nb = q;
         na.y = neg<FqP>(qa.y);
@@ -253,9 +271,10 @@ int main() {
         a = xyzz_madd(a, na);
         b = xyzz_madd_g1(b, nb);
         step(nb);
+        dstep(q, !neg_);
       }
       prev = j;
-      if (!same(a, b) || !same(a, c)) {
+      if (!same(a, b) || !same(a, c) || !same(a, df)) {
         printf("mismatch trial %d step %d\n", trial, s);
         return 1;
       }
@@ -283,6 +302,31 @@ int main() {
           !xyzz_is_inf(xyzz_add_g1(a, neg_a)) != !xyzz_is_inf(xyzz_add(a, neg_a)) ||
           !same(xyzz_add_g1(xyzz_inf<F>(), other), other) || !same(xyzz_add_g1(other, xyzz_inf<F>()), other)) {
         printf("full add mismatch trial %d\n", trial);
+        return 1;
+      }
+    }
+    // xyzz_madd_g1f on a multi-point accumulator: + itself (doubling), + its
+    // negation (borrow-form y: infinity), and the output bounds
+    if (dphase == 2) {
+      Aff<F> s = to_aff(df);
+      bool inf = true;
+      Xyzz<F> dd = xyzz_madd_g1f(df, s.x, s.y, &inf);
+      if (inf || !same(dd, xyzz_mdbl(s))) {
+        printf("madd_g1f doubling mismatch trial %d\n", trial);
+        return 1;
+      }
+      xyzz_madd_g1f(df, s.x, bsub(FqP::B2_1, s.y), &inf);
+      const Fe p8 = fe_const<FqP>(FqP::P8), p2 = fe_const<FqP>(FqP::P2);
+      auto lt = [](const Fe& a, const Fe& b) {
+        for (int i = NL - 1; i >= 0; i--)
+          if (a.v[i] != b.v[i]) return a.v[i] < b.v[i];
+        return false;
+      };
+      bool norm = true;
+      for (int i = 0; i < NL - 1; i++)
+        norm = norm && df.x.v[i] <= LMASK && df.y.v[i] <= LMASK && df.zz.v[i] <= LMASK && df.zzz.v[i] <= LMASK;
+      if (!inf || !norm || !lt(df.x, p8) || !lt(df.y, p2) || !lt(df.zz, p2) || !lt(df.zzz, p2)) {
+        printf("madd_g1f cancellation / bounds mismatch trial %d\n", trial);
         return 1;
       }
     }

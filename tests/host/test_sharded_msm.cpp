@@ -159,6 +159,33 @@ int run_rank(int rank, int dev, Link link, bool use_rccl) {
     int rc = sharded_msm(comm, ctx, rank, 3, 4, 1u << 17, rank == 0, got);
     CHECK(rc == ZKMI_EINVAL, "mismatched plans returned %d", rc);
   }
+  // a rank that fails its local checks (range outside its base set) fails the
+  // MSM on BOTH ranks, and neither blocks in a collective
+  {
+    size_t first = 0, count = 0;
+    zkmi_shard_range(1u << 16, 2, rank, &first, &count);
+    zkmi_bases* b = nullptr;
+    void* d = nullptr;
+    CHECK(zkmi_bases_generate_range_g1(ctx, 5, first, count, &b) == 0 && zkmi_dev_alloc(ctx, count * 32 + 32, &d) == 0 &&
+              zkmi_scalars_generate_range(ctx, 6, first, count, d) == 0,
+          "inputs");
+    uint64_t got[8];
+    int rc = zkmi_msm_sharded(comm, b, rank == 1 ? 1 : 0, d, count, got);  // rank 1: [1, count + 1) out of range
+    CHECK(rc == ZKMI_EINVAL, "bad range on rank 1: rank %d returned %d", rank, rc);
+    // a failure after the plan agreement (injected on rank 0): both fail
+    setenv("ZKMI_DEBUG_SHARD_FAIL", "0", 1);
+    rc = zkmi_msm_sharded(comm, b, 0, d, count, got);
+    unsetenv("ZKMI_DEBUG_SHARD_FAIL");
+    CHECK(rc != 0, "injected failure on rank 0: rank %d returned %d", rank, rc);
+    zkmi_dev_free(ctx, d);
+    zkmi_bases_destroy(b);
+    // the communicator is still in step: a good MSM follows
+    uint64_t want[8] = {0};
+    rc = sharded_msm(comm, ctx, rank, 1026, 26, 1u << 16, false, got);
+    CHECK(rc == 0 && full_msm(ctx, 1026, 26, 1u << 16, want) && memcmp(got, want, sizeof(got)) == 0,
+          "sharded MSM after the failures (rc %d)", rc);
+    if (rank == 0) printf("failure cases: ok\n");
+  }
   zkmi_comm_destroy(comm);
   zkmi_ctx_destroy(ctx);
   return g_fail ? 1 : 0;

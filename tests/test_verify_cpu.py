@@ -200,3 +200,35 @@ def test_bilinearity_against_test_pairing():
     assert PR.pairing_product_is_one([(ap, bq), (abp, q)])
     inp2 = _be_g1(ap) + _be_g2(bq) + _be_g1(g) + _be_g2(q)
     assert alt_bn128("pairing", inp2, 32) == bytes(32)
+
+
+def test_verify_rejects_non_canonical_proof_coordinates():
+    """A coordinate >= q (the same point encoded as x + q) is an invalid
+    proof, as the alt_bn128 syscalls treat it, not silently reduced."""
+    vkb = compressed_vk(ref_vk())
+    (a, b, c), _ = ref_proof()
+    assert verify(vkb, [49], a, b, c) == (0, 1)
+    for arr, k in ((a, 0), (a, 4), (c, 0), (c, 4), (b, 0), (b, 4), (b, 8), (b, 12)):
+        bad = np.array(arr, np.uint64).copy()
+        v = O.limbs_to_int(bad[k:k + 4]) + O.Q
+        if v >= 1 << 256:
+            continue
+        bad[k:k + 4] = O.int_to_limbs(v)
+        args = [a, b, c]
+        args[[id(a), id(b), id(c)].index(id(arr))] = bad
+        assert verify(vkb, [49], *args) == (0, 0)
+
+
+def test_verify_pairing_from_proof_bytes_only():
+    """Groth16Prover.verify_pairing on a BatchProof that carries only its
+    256 proof bytes (deserialized): the points are decoded from -A || B || C."""
+    from zelana_amd import gpu
+    from zelana_amd.prover import proof_points_from_solana_bytes
+    (a, b, c), _ = ref_proof()
+    raw = gpu.proof_to_solana_bytes(a, b, c)
+    a2, b2, c2 = proof_points_from_solana_bytes(raw)
+    assert np.array_equal(a2, np.asarray(a, np.uint64)) and np.array_equal(b2, np.asarray(b, np.uint64))
+    assert np.array_equal(c2, np.asarray(c, np.uint64))
+    with pytest.raises(ValueError):
+        proof_points_from_solana_bytes(raw[:255])
+    assert gpu.groth16_verify(compressed_vk(ref_vk()), [49], a2, b2, c2)

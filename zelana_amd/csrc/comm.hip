@@ -16,6 +16,8 @@
 // the same lane with no host round trip.
 #include <string.h>
 
+#include <vector>
+
 #include <rccl/rccl.h>
 
 #include "zkmi_internal.h"
@@ -69,6 +71,32 @@ int comm_allgather_host(zkmi_comm* c, const void* send, void* recv, size_t bytes
   ZK_NCCL(ncclAllGather(d, d + bytes, bytes, ncclUint8, (ncclComm_t)c->nccl_ctl, c->st_ctl));
   ZK_HIP(hipMemcpyAsync(recv, d + bytes, bytes * c->nranks, hipMemcpyDeviceToHost, c->st_ctl));
   ZK_HIP(hipStreamSynchronize(c->st_ctl));
+  return 0;
+}
+
+int comm_fail_exchange(zkmi_comm* c, size_t words) {
+  if (c->kind == ZKMI_COMM_HOST) {
+    std::vector<uint32_t> me(words, 0), all(words * (size_t)c->nranks);
+    me[words - SHARD_STATUS_WORDS] = 1;
+    return c->fn(c->user, me.data(), all.data(), words * 4) ? ZKMI_EINVAL : 0;
+  }
+  const size_t need = words * (size_t)c->nranks;
+  if (need > c->fail_words) {  // beyond the buffer sized at init: best effort
+    uint32_t* d = nullptr;
+    if (hipMalloc((void**)&d, need * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      return ZKMI_ENOMEM;
+    }
+    if (c->d_fail) (void)hipFree(c->d_fail);
+    c->d_fail = d;
+    c->fail_words = need;
+  }
+  uint32_t* mine = c->d_fail + words * (size_t)c->rank;
+  const uint32_t one = 1;
+  ZK_HIP(hipMemsetAsync(mine, 0, words * 4, c->st));
+  ZK_HIP(hipMemcpyAsync(mine + words - SHARD_STATUS_WORDS, &one, 4, hipMemcpyHostToDevice, c->st));
+  ZK_NCCL(ncclAllGather(mine, c->d_fail, words * 4, ncclUint8, (ncclComm_t)c->nccl, c->st));
+  ZK_HIP(hipStreamSynchronize(c->st));
   return 0;
 }
 
@@ -140,6 +168,15 @@ int zkmi_comm_init(zkmi_ctx* ctx, const uint8_t id[ZKMI_COMM_ID_BYTES], int nran
     return ZKMI_EHIP;
   }
   c->nccl_ctl = ctl;
+  // failure-exchange buffer: 64K words per rank covers every window plan's
+  // bit sums (<= ~24K words for G2)
+  c->fail_words = (size_t)65536 * nranks;
+  if (hipMalloc((void**)&c->d_fail, c->fail_words * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("zkmi_comm_init: cannot allocate the failure-exchange buffer");
+    zkmi_comm_destroy(c);
+    return ZKMI_ENOMEM;
+  }
   *out = c;
   return 0;
 }
@@ -167,6 +204,7 @@ void zkmi_comm_destroy(zkmi_comm* c) {
   if (c->nccl_ctl) ncclCommDestroy((ncclComm_t)c->nccl_ctl);
   if (c->nccl) ncclCommDestroy((ncclComm_t)c->nccl);
   if (c->d_stage) (void)hipFree(c->d_stage);
+  if (c->d_fail) (void)hipFree(c->d_fail);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
   if (c->ev_out) (void)hipEventDestroy(c->ev_out);
   if (c->st) (void)hipStreamDestroy(c->st);

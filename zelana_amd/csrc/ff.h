@@ -50,6 +50,20 @@ struct FqP {
                                       0x11238484u, 0x03e94786u, 0x1628e538u, 0x012259d6u};
   static constexpr uint32_t P8[NL] = {0x03e7ea38u, 0x082305b6u, 0x03951a78u, 0x16a91687u, 0x0c2ecbc0u,
                                       0x16da0605u, 0x05370a08u, 0x12e131a0u, 0x01832273u};
+  // Borrow forms of K p: limbs 0..7 raised by m 2^29 (m borrowed from the next
+  // limb), so that K p - a is limb-wise non-negative for any normalised a
+  // (m = 1) or for a + 2b (m = 3) without a carry pass (BK_m, ec.h
+  // xyzz_madd_g1f).  Same values as K p.
+  static constexpr uint32_t B2_1[NL] = {0x30f9fa8eu, 0x2208c16cu, 0x38e5469du, 0x25aa45a0u, 0x2b0bb2efu,
+                                        0x25b68180u, 0x214dc281u, 0x3cb84c67u, 0x0060c89bu};
+  static constexpr uint32_t B4_1[NL] = {0x21f3f51cu, 0x241182dau, 0x31ca8d3bu, 0x2b548b42u, 0x361765dfu,
+                                        0x2b6d0301u, 0x229b8503u, 0x397098cfu, 0x00c19138u};
+  static constexpr uint32_t B8_1[NL] = {0x23e7ea38u, 0x282305b5u, 0x23951a77u, 0x36a91686u, 0x2c2ecbbfu,
+                                        0x36da0604u, 0x25370a07u, 0x32e1319fu, 0x01832272u};
+  static constexpr uint32_t B6_3[NL] = {0x72edefaau, 0x661a4445u, 0x6aafd3d7u, 0x70fed0e2u, 0x612318cdu,
+                                        0x71238481u, 0x63e94783u, 0x7628e535u, 0x012259d3u};
+  static constexpr uint32_t B10_1[NL] = {0x34e1e4c6u, 0x2a2bc722u, 0x3c7a6115u, 0x3c535c27u, 0x373a7eafu,
+                                         0x3c908785u, 0x2684cc89u, 0x2f997e07u, 0x01e3eb0fu};
 };
 // Scalar field r (NTT domain)
 struct FrP {
@@ -120,6 +134,13 @@ ZK_HD Fe fe_zero() {
 // single wave would see) and pays a 64-bit add per split, ~9% of a
 // multiplication; with 3-4 waves per SIMD the latency is already hidden.
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(ZK_NO_ASM_MAD)
+// The carry-out (unused) goes to a fresh SGPR pair ("=s").  (ZK_MAC_SDST=0
+// writes VCC, declared clobbered, instead: it saves the ~20 SGPR-spill reloads
+// per G1 accumulation step but makes hipcc 8x slower on these files.)
+#ifndef ZK_MAC_SDST
+#define ZK_MAC_SDST 1
+#endif
+#if ZK_MAC_SDST
 __device__ __forceinline__ void mac(uint64_t& acc, uint32_t a, uint32_t b) {
   uint64_t cy;
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cy) : "v"(a), "v"(b));
@@ -129,8 +150,22 @@ __device__ __forceinline__ void macs(uint64_t& acc, uint32_t a, uint32_t b_unifo
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cy) : "v"(a), "s"(b_uniform));
 }
 #else
+__device__ __forceinline__ void mac(uint64_t& acc, uint32_t a, uint32_t b) {
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
+}
+__device__ __forceinline__ void macs(uint64_t& acc, uint32_t a, uint32_t b_uniform) {
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "s"(b_uniform) : "vcc");
+}
+#endif
+// acc += d (32-bit addend) as one v_mad_u64_u32 by the inline constant 1
+__device__ __forceinline__ void mac1(uint64_t& acc, uint32_t d) {
+  uint64_t cy;
+  asm("v_mad_u64_u32 %0, %1, %2, 1, %0" : "+v"(acc), "=s"(cy) : "v"(d));
+}
+#else
 ZK_HD void mac(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b; }
 ZK_HD void macs(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b; }
+ZK_HD void mac1(uint64_t& acc, uint32_t d) { acc += d; }
 #endif
 
 // ------------------------------------------------------------ Montgomery mul
@@ -163,6 +198,98 @@ ZK_HD Fe mul(const Fe& a, const Fe& b) {
     acc >>= 29;
   }
   r.v[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+// r = a*b*2^-261 + d (mod p, lazy): the Montgomery product with d added into
+// its upper columns, so the sum comes out normalised with no carry pass of its
+// own (9 one-instruction adds instead of a 9-limb signed-carry subtraction
+// when d is a borrow-form difference such as 8p - x, FqP::BK_m).  d: limbs
+// 0..7 non-negative and < 2^31; limb 8 is added modulo 2^32 (a borrow there is
+// harmless while the true sum is non-negative).  Value: < a b / R + p + d.
+template <class P>
+ZK_HD Fe mul_add(const Fe& a, const Fe& b, const Fe& d) {
+  uint32_t m[NL];
+  Fe r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      mac(acc, a.v[j], b.v[k - j]);
+      macs(acc, m[j], P::P[k - j]);
+    }
+    mac(acc, a.v[k], b.v[0]);
+    m[k] = ((uint32_t)acc * P::PINV) & LMASK;
+    macs(acc, m[k], P::P[0]);
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+    mac1(acc, d.v[k - NL]);
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) {
+      mac(acc, a.v[j], b.v[k - j]);
+      macs(acc, m[j], P::P[k - j]);
+    }
+    r.v[k - NL] = (uint32_t)acc & LMASK;
+    acc >>= 29;
+  }
+  r.v[NL - 1] = (uint32_t)acc + d.v[NL - 1];
+  return r;
+}
+// r = a^2 * 2^-261 + d, as mul_add
+template <class P>
+ZK_HD Fe sqr_add(const Fe& a, const Fe& d) {
+  uint32_t m[NL], dd[NL];
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) dd[i] = a.v[i] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int j = 0; j < (k + 1) / 2; j++) mac(acc, dd[j], a.v[k - j]);
+    if ((k & 1) == 0) mac(acc, a.v[k / 2], a.v[k / 2]);
+#pragma unroll
+    for (int j = 0; j < k; j++) macs(acc, m[j], P::P[k - j]);
+    m[k] = ((uint32_t)acc * P::PINV) & LMASK;
+    macs(acc, m[k], P::P[0]);
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+    mac1(acc, d.v[k - NL]);
+#pragma unroll
+    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) mac(acc, dd[j], a.v[k - j]);
+    if ((k & 1) == 0) mac(acc, a.v[k / 2], a.v[k / 2]);
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) macs(acc, m[j], P::P[k - j]);
+    r.v[k - NL] = (uint32_t)acc & LMASK;
+    acc >>= 29;
+  }
+  r.v[NL - 1] = (uint32_t)acc + d.v[NL - 1];
+  return r;
+}
+// limb-wise c - a (c a borrow-form constant, a normalised): no carry pass
+ZK_HD Fe bsub(const uint32_t (&c)[NL], const Fe& a) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = c[i] - a.v[i];
+  return r;
+}
+// limb-wise c - a - 2b (c = BK_3)
+ZK_HD Fe bsub2(const uint32_t (&c)[NL], const Fe& a, const Fe& b) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = c[i] - (a.v[i] + (b.v[i] << 1));
+  return r;
+}
+// limb-wise c - a + b (c = BK_1, a and b normalised): limbs < 1.5 2^30
+ZK_HD Fe bsubadd(const uint32_t (&c)[NL], const Fe& a, const Fe& b) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = c[i] - a.v[i] + b.v[i];
   return r;
 }
 

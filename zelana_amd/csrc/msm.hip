@@ -30,6 +30,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <string>
+#include <vector>
 #include <chrono>
 
 #include "dev_io.h"
@@ -1068,13 +1070,102 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
     st_acc<G>(xpts + (size_t)it.w * XW, acc);
   }
 }
+// G1 one-lane-per-item accumulation (the dominant kernel of a table MSM):
+// rows gathered one entry ahead, the first finite point
+// taken as is, the second added by the affine + affine form and every later
+// one by xyzz_madd_g1f (subtractions folded into the Montgomery products).  A
+// negative digit's y is the borrow form 2p - y (9 subtractions, no carry
+// pass), or the -P row of the negated table when there is one.  The rare
+// states (a base at infinity, the empty or one-point accumulator after a
+// cancellation) branch per lane; lanes of a wave have equal trip counts.
+#ifndef ZK_ACC_G1_V1
+#define ZK_ACC_G1_V1 0
+#endif
+__device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
+                                              const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
+                                              const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                                              uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey,
+                                              uint32_t* __restrict__ xvalid, uint32_t* __restrict__ xpts) {
+  using F = FqOps;
+  constexpr int XW = 32;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *nitems) return;
+  const uint4 it = items[i];
+  const uint32_t start = it.x, end = it.y;
+  auto row = [&](uint32_t v) {
+    uint32_t idx = v & 0x7FFFFFFFu;
+    if (tskip) idx += (idx / tn) * tskip;
+    const uint32_t* src = nbases && (v >> 31) ? nbases : bases;  // -P rows for a negative digit
+    return reinterpret_cast<const uint4*>(src + (size_t)idx * G1T::PW);
+  };
+  Xyzz<F> acc = xyzz_inf<F>();
+  int phase = 0;  // 0: nothing yet, 1: acc is one affine point, 2: general
+  auto step = [&](const uint4 (&r)[4], uint32_t v) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(r);
+    if (w[G1T::PW - 1] >> 31) return;  // base at infinity
+    const Fe x2 = unpack(w);
+    const Fe y0 = unpack(w + 8);
+    const Fe yn = bsub(FqP::B2_1, y0);
+    const bool ng = !nbases && (v >> 31);
+    Fe y2;
+#pragma unroll
+    for (int k = 0; k < NL; k++) y2.v[k] = ng ? yn.v[k] : y0.v[k];
+    if (phase == 2) {
+      bool inf;
+      acc = xyzz_madd_g1f(acc, x2, y2, &inf);
+      if (inf) phase = 0;
+    } else if (phase == 1) {
+      acc = xyzz_mmadd_g1({acc.x, acc.y}, Aff<F>{x2, reduce_q32<FqP>(y2)});
+      phase = xyzz_is_inf(acc) ? 0 : 2;
+    } else {
+      acc = xyzz_from_aff(Aff<F>{x2, reduce_q32<FqP>(y2)});
+      phase = 1;
+    }
+  };
+  // one call site of the addition (each inlined copy is ~3.5K instructions):
+  // the row of entry p + 1 is in flight while entry p is added.  The loads
+  // are unconditional (past the end they re-read the last entry), so the
+  // buffer is one loop-carried value with a single copy per entry.
+  uint4 raw[4];
+  const uint32_t last = end - 1;
+  uint32_t v_nxt = sval[start];
+  {
+    const uint4* q = row(v_nxt);
+#pragma unroll
+    for (int k = 0; k < 4; k++) raw[k] = q[k];
+  }
+  uint32_t v_nn = sval[min(start + 1, last)];
+  for (uint32_t p = start; p < end; p++) {
+    uint4 cr[4];
+    const uint32_t v = v_nxt;
+#pragma unroll
+    for (int k = 0; k < 4; k++) cr[k] = raw[k];
+    {
+      const uint4* q = row(v_nn);
+#pragma unroll
+      for (int k = 0; k < 4; k++) raw[k] = q[k];
+    }
+    v_nxt = v_nn;
+    v_nn = sval[min(p + 2, last)];
+    step(cr, v);
+  }
+  if (phase == 0) acc = xyzz_inf<F>();
+  if (it.w == NOSLOT) {
+    st_acc<G1T>(buckets + (size_t)it.z * XW, acc);
+  } else {
+    xkey[it.w] = it.z;
+    xvalid[it.w] = 1;
+    st_acc<G1T>(xpts + (size_t)it.w * XW, acc);
+  }
+}
 __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
     k_acc_items_g1(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
                    const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                    uint32_t* __restrict__ xpts) {
-  acc_items_body<G1T>(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts);
+  if constexpr (ZK_ACC_G1_V1) acc_items_body<G1T>(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts);
+  else acc_items_g1f(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts);
 }
 __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
     k_acc_items_g2(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
@@ -1505,6 +1596,76 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
     uint32_t* dst = (rows ? outC : outD) + (size_t)ln * XW;
     for (int k = 0; k < XW; k++) dst[k] = src[k];
   }
+}
+
+// Mode 3, second pass: the k_br_fold partials of a line summed by one wave
+// (rows: 64 lanes, contiguous strips of 2^lb / S / 64 partials) or by mc lanes
+// (columns: 64 / mc columns per wave), then the in-wave tree of
+// k_msm_br_strip.  Outputs C[w][h], D[w][l] (sr = sc = 1).  k_br_fold runs
+// every addition of the first pass at full occupancy (one lane per S buckets,
+// 2^18 lanes at 2^19 buckets); only this pass and the bit sums are
+// latency-bound, and they hold one wave per SIMD at most.
+template <class G>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE)))
+    k_br_strip_p(const uint32_t* __restrict__ part, int lb, int hb, int W, int S, int mc, uint32_t* __restrict__ outC,
+                 uint32_t* __restrict__ outD) {
+  using F = typename G::F;
+  constexpr int XW = 4 * G::CW;
+  __shared__ Xyzz<F> sh[4][32];
+  const int bb = lb + hb;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t job = blockIdx.x * 4 + wave;
+  const uint32_t nrow = (uint32_t)W << hb, ncol = (uint32_t)W << lb;
+  const uint32_t Lr = (1u << lb) / S, Lc = (1u << hb) / S;  // partials per row / column line
+  const uint32_t cpw = 64u / (uint32_t)mc;
+  const bool row_wave = job < nrow;
+  const uint32_t m = row_wave ? 64u : (uint32_t)mc;
+  const uint32_t sub = lane & (m - 1), lslot = (lane / m) * (m / 2);
+  bool live = false;
+  size_t base = 0, stride = 1;
+  uint32_t len = 0;
+  uint32_t* dst = nullptr;
+  if (row_wave) {
+    live = true;
+    len = Lr;
+    base = (size_t)job * Lr;
+    dst = outC + (size_t)job * XW;
+  } else {
+    const uint32_t jj = (job - nrow) * cpw + lane / m;  // (w << lb) + l
+    if (jj < ncol) {
+      const uint32_t w = jj >> lb, l = jj & ((1u << lb) - 1);
+      live = true;
+      len = Lc;
+      base = ((size_t)W << bb) / S + (((size_t)w * Lc) << lb) + l;
+      stride = (size_t)1 << lb;
+      dst = outD + (size_t)jj * XW;
+    }
+  }
+  const uint32_t L = (len + m - 1) / m;
+  const uint32_t Lmax = ((Lr + 63) / 64) > ((Lc + mc - 1) / mc) ? (Lr + 63) / 64 : (Lc + mc - 1) / mc;
+  Xyzz<F> v = xyzz_inf<F>();
+  for (uint32_t step = 0; step < Lmax + 6; step++) {
+    Xyzz<F> q;
+    bool act = false;
+    if (step < Lmax) {
+      const uint32_t t = sub * L + step;
+      if (live && step < L && t < len) {
+        q = ld_xyzz<G>(part + (base + (size_t)t * stride) * XW);
+        act = !xyzz_is_inf(q);
+      }
+    } else {
+      const uint32_t sz = 32u >> (step - Lmax);
+      if (sz < m && sub >= sz && sub < 2 * sz) sh[wave][lslot + sub - sz] = v;
+      __syncthreads();
+      if (sz < m && sub < sz) {
+        q = sh[wave][lslot + sub];
+        act = !xyzz_is_inf(q);
+      }
+    }
+    if (act) v = xyzz_is_inf(v) ? q : br_add<G>(v, q);
+    if (step >= Lmax) __syncthreads();
+  }
+  if (live && sub == 0) st_xyzz<G>(dst, v);
 }
 
 // ------------------------------------------------------------ base upload
@@ -2183,6 +2344,8 @@ struct zkmi_msm_job {
   int sb = 1;                   // segments per bit sum (added on the host)
   hipStream_t st = nullptr;     // lane stream the D2H of `host` is queued on
   zkmi_comm* comm = nullptr;    // sharded MSM: bit sums of every rank are summed
+  size_t status_words = 0;      // sharded: status block after the bit sums (per rank)
+  bool exchanged = false;       // sharded over RCCL: the data all-gather is queued
 };
 
 namespace zk {
@@ -2416,12 +2579,18 @@ static BrGeom br_geom(const MsmPlan& P, bool g2) {
     return e ? atoi(e) : 0;
   }();
   BrGeom g;
-  g.mode = P.hb >= 9 ? (env_mode == 2 ? 2 : 1) : 0;
+  g.mode = P.hb >= 9 ? (env_mode == 2 || env_mode == 3 ? env_mode : 1) : 0;
   g.S = env_fold == 4 ? 4 : 8;
   g.segt = env_seg == 64 || env_seg == 128 ? env_seg : 256;
   if (g.mode == 2) {
     g.sr = g.sc = 1;
     g.segt = env_seg == 64 || env_seg == 256 ? env_seg : 128;
+  } else if (g.mode == 3) {
+    g.sr = g.sc = 1;
+    g.S = env_fold == 8 ? 8 : 4;
+    const int lenc = (1 << P.hb) / g.S;  // column partials per line
+    g.mc = 64;
+    while (g.mc > 1 && lenc / g.mc < 4) g.mc >>= 1;
   } else {
     const int fold = g2 ? strip_fold2 : strip_fold;
     const int segb = g.mode == 1 ? 64 * fold : 256;  // buckets per wave job
@@ -2446,10 +2615,16 @@ static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, hipStream_t st, zkmi
   const int nr = job->comm ? job->comm->nranks : 1;
   const bool dev_gather = job->comm && job->comm->kind == ZKMI_COMM_RCCL;
   const uint32_t* src = d_sums;
+  if (job->comm) {  // sharded: a zero status block ends this rank's payload (d_sums has room)
+    ZK_HIP(hipMemsetAsync(const_cast<uint32_t*>(d_sums) + words, 0, SHARD_STATUS_WORDS * 4, st));
+    words += SHARD_STATUS_WORDS;
+    job->status_words = SHARD_STATUS_WORDS;
+  }
   if (dev_gather) {
     uint32_t* gathered;
     ZK_TRY(lane->ws.get("msm_gathered", (size_t)nr * words * 4, (void**)&gathered));
     ZK_TRY(comm_allgather_device(job->comm, st, d_sums, gathered, words * 4));
+    job->exchanged = true;
     src = gathered;
   }
   job->host_words = words;
@@ -2589,7 +2764,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   const int sr = bg.sr, sc = bg.sc, sb = bg.sb;
   ZK_TRY(ws.get("msm_C", (size_t)W * (1u << hb) * sr * XW * 4, (void**)&Cb));
   ZK_TRY(ws.get("msm_D", (size_t)W * (1u << lb) * sc * XW * 4, (void**)&Db));
-  ZK_TRY(ws.get("msm_sums", (size_t)W * (bb + 1) * sb * XW * 4, (void**)&sums));
+  ZK_TRY(ws.get("msm_sums", ((size_t)W * (bb + 1) * sb * XW + SHARD_STATUS_WORDS) * 4, (void**)&sums));
   if (!(debug_skip() & 4)) {
     ScopedKernelTimer tm(ctx, "msm_bucket_reduce", brs);
     uint32_t jobs2 = (uint32_t)W * (bb + 1) * sb;
@@ -2603,6 +2778,16 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       auto wgs = [](uint32_t lines, uint32_t len) { return len >= 256 ? lines : lines / (256 / len); };
       const uint32_t nwr = wgs((uint32_t)W << hb, (1u << lb) / bg.S), nwc = wgs((uint32_t)W << lb, (1u << hb) / bg.S);
       k_br_lines<G><<<nwr + nwc, 256, 256 * XW * 4, brs>>>(part, lb, hb, W, bg.S, nwr, Cb, Db);
+    } else if (bg.mode == 3) {
+      const uint32_t nstrips = (uint32_t)W * ((1u << bb) / bg.S);  // per direction
+      uint32_t* part;
+      ZK_TRY(ws.get("msm_brpart", (size_t)2 * nstrips * XW * 4, (void**)&part));
+      const unsigned g1 = (2 * nstrips + 255) / 256;
+      if (bg.S == 8) k_br_fold<G, 8><<<g1, 256, 0, brs>>>(buckets, bstart, lb, hb, W, part);
+      else k_br_fold<G, 4><<<g1, 256, 0, brs>>>(buckets, bstart, lb, hb, W, part);
+      const uint32_t nrow = (uint32_t)W << hb, ncol = (uint32_t)W << lb, cpw = 64u / (uint32_t)bg.mc;
+      const uint32_t jobs1 = nrow + (ncol + cpw - 1) / cpw;
+      k_br_strip_p<G><<<(jobs1 + 3) / 4, 256, 0, brs>>>(part, lb, hb, W, bg.S, bg.mc, Cb, Db);
     } else if (bg.mode == 1) {  // one wave per row segment, 64 / mc column segments per wave
       const uint32_t nrow = (uint32_t)W * ((1u << hb) * sr), ncol = (uint32_t)W * ((1u << lb) * sc);
       const uint32_t cpw = 64u / (uint32_t)bg.mc;
@@ -2733,6 +2918,8 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
   hipError_t e = hipEventSynchronize(job->done);
   if (e != hipSuccess) {
     set_error("msm_wait: %s", hipGetErrorString(e));
+    // a host-transport peer waits for this rank's bit sums: hand it a failure
+    if (job->comm && job->comm->kind == ZKMI_COMM_HOST) (void)comm_fail_exchange(job->comm, job->host_words);
     job->host = nullptr;  // copy state unknown: never recycle the buffer
     msm_job_free(job);
     return ZKMI_EHIP;
@@ -2754,6 +2941,15 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
       return grc;
     }
     src = gathered.data();
+  }
+  if (job->comm) {  // every rank's status block: one failed rank fails the MSM everywhere
+    for (int r = 0; r < nr; r++) {
+      if (src[(size_t)r * job->host_words + job->host_words - job->status_words] != 0) {
+        set_error("msm_sharded: rank %d failed while running its shard", r);
+        msm_job_free(job);
+        return ZKMI_EINVAL;
+      }
+    }
   }
   // terms: V_{c w + j} = U_{w,j} (j < c-1), then T_w at weight 2^{c w}
   // (each term arrives as sb segments per rank, all summed in the combine)
@@ -2792,23 +2988,40 @@ int msm_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_
 // pipeline, and the job hands over the bit sums of all ranks (msm_wait sums
 // them).  A rank with an empty shard contributes the same number of infinity
 // terms, so the collective still matches on every rank.
+// Failures never strand a peer inside a collective: every rank joins the
+// header exchange with its local validation result (hdr[6]) and all fail
+// together if one does; a rank that fails after the agreement still takes
+// part in the job's data exchange with its status word set
+// (comm_fail_exchange), so the others fail in msm_wait.
 int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                        zkmi_msm_job** out) {
   *out = nullptr;
-  ZK_TRY(check_range(b, offset, n));
   zkmi_ctx* ctx = comm->ctx;
-  if (b->ctx != ctx) {
+  int lrc = check_range(b, offset, n);
+  if (!lrc && b->ctx != ctx) {
     set_error("msm_sharded: base set belongs to another context than the communicator");
-    return ZKMI_EINVAL;
+    lrc = ZKMI_EINVAL;
   }
-  const MsmPlan P = msm_plan(ctx, b, n);
-  const BrGeom bg = br_geom(P, b->g2 != 0);
+  MsmPlan P{};
+  BrGeom bg{};
+  if (!lrc) {
+    P = msm_plan(ctx, b, n);
+    bg = br_geom(P, b->g2 != 0);
+    if (n) lrc = check_size(P, n);
+  }
+  const std::string lerr = lrc ? std::string(zkmi_last_error()) : std::string();
   constexpr uint32_t MAGIC = 0x5A4B4D53u;
-  uint32_t hdr[8] = {MAGIC, (uint32_t)b->g2, n ? (uint32_t)P.c : 0u, n ? (uint32_t)P.W : 0u,
-                     n ? (uint32_t)P.bb : 0u, n ? (uint32_t)bg.sb : 0u, 0u, 0u};
-  if (n) ZK_TRY(check_size(P, n));
+  const bool plan = !lrc && n;
+  uint32_t hdr[8] = {MAGIC, b ? (uint32_t)b->g2 : 0u, plan ? (uint32_t)P.c : 0u, plan ? (uint32_t)P.W : 0u,
+                     plan ? (uint32_t)P.bb : 0u, plan ? (uint32_t)bg.sb : 0u, lrc ? 1u : 0u, 0u};
   std::vector<uint32_t> all((size_t)8 * comm->nranks);
   ZK_TRY(comm_allgather_host(comm, hdr, all.data(), sizeof(hdr)));
+  for (int r = 0; r < comm->nranks; r++) {
+    if (all[(size_t)8 * r + 6] == 0) continue;
+    if (lrc) set_error("%s", lerr.c_str());
+    else set_error("msm_sharded: rank %d failed its local checks", r);
+    return ZKMI_EINVAL;
+  }
   const uint32_t* ref = nullptr;
   for (int r = 0; r < comm->nranks; r++) {
     const uint32_t* h = &all[(size_t)8 * r];
@@ -2836,19 +3049,26 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
   job->W = (int)ref[3];
   job->bb = (int)ref[4];
   job->sb = (int)ref[5];
+  const int XW = b->g2 ? 64 : 32;
+  const size_t words = (size_t)job->W * (job->bb + 1) * job->sb * XW;  // bit sums per rank
   int rc = 0;
   MsmLane* lane = nullptr;
-  if (n) {
+  // test hook (tests/host/test_sharded_msm.cpp): ZKMI_DEBUG_SHARD_FAIL=<rank>
+  // makes that rank fail after the plan agreement, before its exchange
+  const char* dbg = getenv("ZKMI_DEBUG_SHARD_FAIL");
+  if (dbg && atoi(dbg) == comm->rank) {
+    set_error("msm_sharded: injected failure (ZKMI_DEBUG_SHARD_FAIL)");
+    rc = ZKMI_EHIP;
+  } else if (n) {
     uint32_t *sval, *bstart;
     if (!(rc = get_lane(ctx, &lane)) && !(rc = msm_sort_phase(ctx, lane, P, (const uint32_t*)d_scalars, n, &sval,
                                                                &bstart)))
       rc = msm_acc_any(ctx, lane, P, b, offset, n, sval, bstart, job);
   } else {
-    // infinity terms (all-zero XYZZ) of the agreed shape
-    const int XW = b->g2 ? 64 : 32;
-    const size_t words = (size_t)job->W * (job->bb + 1) * job->sb * XW;
+    // infinity terms (all-zero XYZZ) of the agreed shape, and the status block
     uint32_t* zeros = nullptr;
-    if (!(rc = get_lane(ctx, &lane)) && !(rc = lane->ws.get("msm_zero_terms", words * 4, (void**)&zeros))) {
+    if (!(rc = get_lane(ctx, &lane)) &&
+        !(rc = lane->ws.get("msm_zero_terms", (words + SHARD_STATUS_WORDS) * 4, (void**)&zeros))) {
       if (hipMemsetAsync(zeros, 0, words * 4, lane->st) != hipSuccess) {
         (void)hipGetLastError();
         set_error("msm_sharded: hipMemsetAsync failed");
@@ -2859,6 +3079,17 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
     }
   }
   if (rc) {
+    // the peers are in (or heading for) this job's data exchange: join it with
+    // a failure status unless this rank's share is already queued (RCCL)
+    if (!job->exchanged && comm->kind == ZKMI_COMM_RCCL) {
+      const std::string err = zkmi_last_error();
+      (void)comm_fail_exchange(comm, words + SHARD_STATUS_WORDS);
+      set_error("%s", err.c_str());
+    } else if (comm->kind == ZKMI_COMM_HOST) {
+      const std::string err = zkmi_last_error();
+      (void)comm_fail_exchange(comm, words + SHARD_STATUS_WORDS);
+      set_error("%s", err.c_str());
+    }
     msm_job_free(job);
     return rc;
   }

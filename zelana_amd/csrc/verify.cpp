@@ -581,6 +581,13 @@ int zkmi_groth16_verify(const uint8_t* vk_bytes, size_t vk_len, const uint64_t* 
     set_error("zkmi_groth16_verify: %zu public inputs for a key with %zu IC points", n_inputs, vk.ic.size());
     return ZKMI_EINVAL;
   }
+  // every proof coordinate must be canonical (< q): from_canon would reduce a
+  // non-canonical encoding silently and accept it (the alt_bn128 entry points
+  // refuse such inputs too)
+  for (int i = 0; i < 2; i++)
+    if (!lt_q(a + 4 * i) || !lt_q(c + 4 * i)) return 0;  // invalid proof
+  for (int i = 0; i < 4; i++)
+    if (!lt_q(b + 4 * i)) return 0;
   G1 A = g1_from_canon(a), C = g1_from_canon(c);
   G2 B = g2_from_canon(b);
   if (!g1_on_curve(A) || !g1_on_curve(C) || !g2_on_curve(B) || !g2_in_subgroup(B)) return 0;  // invalid proof

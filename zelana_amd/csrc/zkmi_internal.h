@@ -108,6 +108,10 @@ struct zkmi_comm {
   size_t stage_bytes = 0;
   zkmi_allgather_fn fn = nullptr;       // host transport
   void* user = nullptr;
+  // RCCL: device buffer (nranks x fail_words) for the failure exchange of a
+  // sharded MSM that fails after its plan was agreed (comm_fail_exchange)
+  uint32_t* d_fail = nullptr;
+  size_t fail_words = 0;
 };
 
 namespace zk {
@@ -119,6 +123,13 @@ int comm_allgather_device(zkmi_comm* c, hipStream_t lane_st, const void* d_send,
 int comm_allgather_host(zkmi_comm* c, const void* send, void* recv, size_t bytes);
 int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                        zkmi_msm_job** out);
+// A rank whose sharded MSM fails after the plan exchange still takes part in
+// the job's data exchange (`words` u32 per rank, the last 4 a status block),
+// with its status word set, so the other ranks fail in their msm_wait instead
+// of blocking in the collective.  Synchronous; issue order as the exchange.
+int comm_fail_exchange(zkmi_comm* c, size_t words);
+// words of the status block that ends every rank's sharded exchange payload
+constexpr size_t SHARD_STATUS_WORDS = 4;
 
 // HIP's current device is per host thread (default 0).  Every entry point that
 // works on a context, key or base set selects that context's device for the

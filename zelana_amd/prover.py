@@ -189,8 +189,12 @@ class Groth16Prover:
         """The on-chain verifier's check (verifier lib.rs:497-547) on the host:
         e(A,B) = e(alpha,beta) e(vk_x,gamma) e(C,delta) under this prover's VK
         (zkmi_groth16_verify).  public_inputs: the circuit's instance values
-        (ints), without the leading One."""
-        return gpu.groth16_verify(self.verifying_key, public_inputs, proof.a, proof.b, proof.c)
+        (ints), without the leading One.  A proof carrying only proof_bytes
+        (e.g. deserialized) is decoded from them, as batch_prover.cpp does."""
+        a, b, c = proof.a, proof.b, proof.c
+        if a is None or b is None or c is None:
+            a, b, c = proof_points_from_solana_bytes(proof.proof_bytes)
+        return gpu.groth16_verify(self.verifying_key, public_inputs, a, b, c)
 
     def verification_key_hash(self) -> bytes:
         return self.vk_hash
@@ -209,6 +213,26 @@ class Groth16Prover:
 
     def export_vk_json(self) -> str:
         return json.dumps({"verifying_key": base64.b64encode(self.verifying_key).decode()}, indent=2)
+
+
+_Q = 0x30644e72e131a029b85045b68181585d97816a916871ca8d3c208c16d87cfd47
+
+
+def proof_points_from_solana_bytes(proof_bytes: bytes):
+    """Undo proof_to_solana_bytes (prover.rs:304-334): -A || B || C, 256 bytes
+    of little-endian coordinates; returns canonical (a, b, c) as uint64 limb
+    arrays with A's y negated back.  Raises ValueError on a wrong length."""
+    import numpy as np
+    raw = bytes(proof_bytes)
+    if len(raw) != 256:
+        raise ValueError(f"proof_bytes must be 256 bytes, got {len(raw)}")
+    w = np.frombuffer(raw, "<u8").copy()
+    a, b, c = w[0:8].copy(), w[8:24].copy(), w[24:32].copy()
+    y = sum(int(a[4 + i]) << (64 * i) for i in range(4))
+    if y:
+        y = _Q - y
+        a[4:8] = [(y >> (64 * i)) & ((1 << 64) - 1) for i in range(4)]
+    return a, b, c
 
 
 def default_l2_synthesizer():
