@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--no-plain", action="store_true", help="skip the no-table side measurement")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: every usable core)")
     ap.add_argument("--no-cpu-prove", action="store_true", help="skip the CPU baseline's zelana_batch proof leg")
+    ap.add_argument("--no-cpu-big", action="store_true", help="skip the CPU baseline's 2^26 MSM leg (~40 s)")
     ap.add_argument("--no-ntt", action="store_true", help="skip the NTT 2^24 side measurement")
     ap.add_argument("--ntt-log-n", type=int, default=24)
     ap.add_argument("--no-l2", action="store_true", help="skip the L2 proof throughput side measurement")
@@ -104,9 +105,14 @@ def main():
     ctx = Context(gpu_index)
     comm = None
     if dist is not None:
-        from zelana_amd.dist import make_comm
+        from zelana_amd.dist import CommInitError, make_comm
 
-        comm = make_comm(ctx, backend)  # libzkmi's own communicator: RCCL, or host (gloo rehearsal)
+        try:
+            comm = make_comm(ctx, backend)  # libzkmi's own communicator: RCCL, or host (gloo rehearsal)
+        except CommInitError as e:  # raised on every rank together: exit non-zero, never hang
+            print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+            sys.exit(1)
     n = 1 << args.log_n
     bases, scalars = msm_inputs(ctx, args.inputs, 20 + rank, 1020 + rank, n, splitmix_point_seed=1000 + rank)
     dev = torch.device("cuda", gpu_index) if torch.cuda.is_available() else None
@@ -131,6 +137,14 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=_coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
+
+    def allgather(x):
+        """every rank's value (list indexed by rank)"""
+        if dist is None:
+            return [x]
+        out = [None] * world
+        dist.all_gather_object(out, x)
+        return out
 
     ctx.set_lanes(args.lanes)
 
@@ -220,9 +234,15 @@ def main():
     ctx.set_lanes(2)
     if not args.no_big:
         log("config 5: global 2^%d MSM" % args.big_log_n)
+        big_state = {} if (rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_cpu_big) else None
         extra["msm_global_2_%d" % args.big_log_n] = bench_msm_sharded(
-            ctx, args.big_log_n, args.big_steps, world, rank, submit, finish, sync_all, allmax, 2, args.inputs)
+            ctx, args.big_log_n, args.big_steps, world, rank, submit, finish, sync_all, allmax, 2, args.inputs,
+            allgather, big_state)
+        if comm is not None:
+            extra["msm_exchange"]["per_rank"] = extra["msm_global_2_%d" % args.big_log_n].get("per_rank")
     ntt_state = zb_state = None
+    if args.no_big:
+        big_state = None
     if not args.no_ntt:
         log("NTT + INTT")
         extra["ntt"], ntt_state = bench_ntt(ctx, args.ntt_log_n, world, sync_all, allmax)
@@ -240,7 +260,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baseline legs")
         cpu = cpu_baseline(ctx, bases, scalars, n, result, args.cpu_threads, ntt_state,
-                           None if args.no_cpu_prove else zb_state, c1_state)
+                           None if args.no_cpu_prove else zb_state, c1_state, big_state)
 
     pmc = pmc_record(kernel, args.log_n)
     traffic = pmc.get("hbm_bytes")
@@ -346,7 +366,8 @@ def msm_inputs(ctx, kind, scalar_seed, point_seed, n, first=0, splitmix_point_se
             ctx.scalars_generate(seed=scalar_seed, n=n, first=first))
 
 
-def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_all, allmax, lanes=2, inputs="stdrng"):
+def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_all, allmax, lanes=2, inputs="stdrng",
+                      allgather=None, keep=None):
     """BASELINE.json configs[4]: ONE global BN254 G1 MSM of 2^log_total
     point-scalar pairs, point-sharded over the world's ranks (strong scaling:
     rank r owns elements [r*N/W, (r+1)*N/W) of the same global set, resident
@@ -376,8 +397,38 @@ def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_a
     t0 = time.perf_counter()
     res = run(steps)
     sync_all()
-    dt = allmax(time.perf_counter() - t0)
+    own = time.perf_counter() - t0
+    dt = allmax(own)
+    # per-rank record (a separate profiled pass: the timers' events cost
+    # throughput): this rank's MSM time, its sort / accumulation / bucket
+    # reduction, and its exchange (ncclAllGather span on the comm stream, HIP
+    # events; host transport: the all-gather call) -- makes the first N-rank
+    # RCCL run diagnosable
+    ctx.profile(True)
+    ctx.profile_reset()
+    sync_all()
+    t1 = time.perf_counter()
+    run(steps)
+    sync_all()
+    prof_own = time.perf_counter() - t1
+    ctx.profile(False)
+
+    def per_ms(name):
+        t, c = ctx.profile_get(name)
+        return round(t / steps, 3) if c else None
+    mine = {"rank": rank, "ms_per_msm": round(own / steps * 1e3, 3),
+            "profiled_ms_per_msm": round(prof_own / steps * 1e3, 3),
+            "exchange_ms_per_msm": per_ms("msm_exchange"), "sort_ms": per_ms("msm_sort"),
+            "acc_ms": per_ms("msm_acc0_g1"), "bucket_reduce_ms": per_ms("msm_bucket_reduce"),
+            "host_epilogue_ms": per_ms("msm_host_epilogue")}
+    ranks = allgather(mine) if allgather else [mine]
     ctx.set_lanes(prev_lanes)
+    if keep is not None and world == 1:  # host copies for the CPU 2^26 leg (cpu_baseline.legs.msm_2_26)
+        keep["log_n"] = log_total
+        keep["pts"] = bases.export()
+        keep["sc"] = np.zeros((per, 4), np.uint64)
+        scalars.download(keep["sc"])
+        keep["res"] = np.array(res, copy=True)
     del bases, scalars
     return {
         "workload": f"BN254 G1 MSM 2^{log_total} (BASELINE.json configs[4]): one global MSM point-sharded over "
@@ -393,6 +444,7 @@ def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_a
         "table": {"window": info[1], "copies": info[2], "build_s": round(table_s, 2)},
         "generate_s": round(gen_s, 2),
         "result_sha256": hashlib.sha256(np.ascontiguousarray(res).tobytes()).hexdigest()[:16],
+        "per_rank": ranks,
     }
 
 
@@ -835,10 +887,12 @@ def host_cores():
     return cores, {"host_cpus": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "cpu_model": model}
 
 
-def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb_state=None, c1_state=None):
+def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb_state=None, c1_state=None,
+                 big_state=None):
     """oracle/ restatement of arkworks on this box's host cores, same inputs
     as the GPU legs, each leg checked for equality with the GPU output:
       msm   ark-ec msm_bigint_wnaf on the headline's 2^20 bases / scalars
+      msm_2_26  the same on config 5's global 2^26 MSM
       ntt   ark-poly radix-2 forward + inverse at 2^24 (configs[2])
       prove ark-groth16 prove of zelana_batch batch 70 (configs[3]) under the
             oracle's own StdRng(0) key (setup untimed), same r and s."""
@@ -939,6 +993,21 @@ def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb
                                     and np.array_equal(c, gc)),
         }
         del keep, keep0, orng
+    if big_state:
+        log("CPU 2^%d MSM leg" % big_state["log_n"])
+        pts, sc = big_state["pts"], big_state["sc"]
+        t0 = time.perf_counter()
+        want = O.msm_g1(pts, sc, threads=threads)
+        dtb = time.perf_counter() - t0
+        nb = sc.shape[0]
+        out["legs"]["msm_2_%d" % big_state["log_n"]] = {
+            "value": round(nb / dtb / 1e6, 3), "unit": "Mpoint-scalar/s", "s_per_msm": round(dtb, 2),
+            "cores": threads, "kind": "port",
+            "sample": f"the full global 2^{big_state['log_n']} MSM of extra.msm_global_2_{big_state['log_n']} (same "
+                      "StdRng(26) scalars and P0 + i*D points), once; ark-ec msm_bigint_wnaf restated, pthreads",
+            "gpu_matches_cpu": bool(np.array_equal(big_state["res"], want)),
+        }
+        big_state.clear()
     return out
 
 

@@ -40,7 +40,10 @@ int comm_allgather_device(zkmi_comm* c, hipStream_t lane_st, const void* d_send,
   }
   ZK_HIP(hipEventRecord(c->ev_in, lane_st));
   ZK_HIP(hipStreamWaitEvent(c->st, c->ev_in, 0));
-  ZK_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, (ncclComm_t)c->nccl, c->st));
+  {
+    ScopedKernelTimer tm(c->ctx, "msm_exchange", c->st);  // per-rank exchange time (zkmi_profile)
+    ZK_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, (ncclComm_t)c->nccl, c->st));
+  }
   ZK_HIP(hipEventRecord(c->ev_out, c->st));
   ZK_HIP(hipStreamWaitEvent(lane_st, c->ev_out, 0));
   return 0;

@@ -2935,7 +2935,13 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
   std::vector<uint32_t> gathered;
   if (job->comm && job->comm->kind == ZKMI_COMM_HOST) {
     gathered.resize((size_t)nr * job->host_words);
+    const auto tx = std::chrono::steady_clock::now();
     int grc = comm_allgather_host(job->comm, job->host, gathered.data(), job->host_words * 4);
+    if (ctx->timer.enabled) {  // per-rank exchange time, as the RCCL path's event timer
+      auto& t = ctx->timer.totals["msm_exchange"];
+      t.first += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tx).count();
+      t.second += 1;
+    }
     if (grc) {
       msm_job_free(job);
       return grc;

@@ -35,18 +35,41 @@ def torch_allgather(group=None):
     return ag
 
 
+class CommInitError(RuntimeError):
+    """libzkmi communicator creation failed on at least one rank."""
+
+
 def make_comm(ctx, backend: str) -> Comm:
     """libzkmi communicator over the current torch.distributed world:
     RCCL when the backend is nccl (the unique id is broadcast by rank 0),
-    otherwise the host transport over torch.distributed."""
+    otherwise the host transport over torch.distributed.
+
+    Every rank reports whether its zkmi_comm_init succeeded (an object
+    all-gather over torch.distributed), so a failure on one rank raises
+    CommInitError with that rank's error text on EVERY rank instead of leaving
+    the others to block in the first collective."""
     import torch.distributed as dist
 
     world, rank = dist.get_world_size(), dist.get_rank()
-    if backend == "nccl":
-        obj = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        return Comm.rccl(ctx, obj[0], world, rank)
-    return Comm.host(ctx, world, rank, torch_allgather())
+    comm, err = None, None
+    try:
+        if backend == "nccl":
+            obj = [comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            comm = Comm.rccl(ctx, obj[0], world, rank)
+        else:
+            comm = Comm.host(ctx, world, rank, torch_allgather())
+    except Exception as e:  # noqa: BLE001 - reported to every rank below
+        err = f"{type(e).__name__}: {e}"
+    errs = [None] * world
+    dist.all_gather_object(errs, err)
+    bad = [(r, e) for r, e in enumerate(errs) if e]
+    if bad:
+        if comm is not None:
+            comm.close()
+        raise CommInitError("libzkmi communicator init failed: " +
+                            "; ".join(f"rank {r}: {e}" for r, e in bad))
+    return comm
 
 
 def allgather_points(point: np.ndarray, device=None) -> list[np.ndarray]:
