@@ -303,6 +303,18 @@ int zkmi_proof_serialize_compressed(const uint64_t a[8], const uint64_t b[16], c
  *         3 BITS64 z[out+i] = bit i of <a,z>; 4 PERM MiMC permutation of
  *         <a,z>: z[out + 4r + (0..3)] = t_r^2, t_r^4, t_r^6, t_r^7 (91 rounds,
  *         t_0 = <a,z> + c_0, t_r = t_{r-1}^7 + c_r, c_i = (i+1)^3 + (i+1))
+ *         5 BITS z[out+i] = bit i of <a,z>, i < b_off (1..256; b_len = 0);
+ *         6 NEQ z[out] = (<a,z> != 0), z[out+1] = <a,z>^-1, or 1 when it is 0
+ *         (r1cs-std is_neq's two witnesses);
+ *         7 POSEIDON one permutation of L2BlockCircuit's width-3 Poseidon
+ *         sponge (prover/src/l2_circuit.rs:68-83: x^5, 8 full + 56 partial
+ *         rounds).  State in: three combinations stored back to back at
+ *         a_off, of lengths a_len, b_len and b_off & 0xFFFF; mask = b_off >> 16
+ *         (1..7) marks the elements that are variables in round 0.  Out: x^2,
+ *         x^4, x^5 of every S-box in round order (round 0 only for masked
+ *         elements): 3 popcount(mask) + 231 values.  Reads the round
+ *         constants ark[r][i] at coefficient 3r + i and the MDS matrix
+ *         m[i][j] at 192 + 3i + j (so num_coeffs >= 201)
  *   term: 2 x u32 {z index, coefficient index}; <a,z> = sum over
  *         term[a_off .. a_off + a_len) of coeff * z
  *   levels: ops [level_start[l], level_start[l+1]) depend only on inputs and

@@ -6,6 +6,11 @@ The GPU proof must equal the oracle's proof on the same R1CS, z and r, s
 (StdRng::seed_from_u64(batch_id)), for an honest batch and for the
 reference's usual unsatisfied one (blake3 batch hash).
 The R1CS itself is parity-unpinned (see l2block.py).
+
+The GPU witness program of the circuit (wprog.hip MUL/BITS/NEQ/POSEIDON ops,
+recorded by the C++ synthesizer) must write the host synthesis's z element for
+element, and the drop-in C++ prover, which runs it for every batch after the
+first of a shape, must give the same proof bytes as the host-synthesis path.
 """
 import numpy as np
 import pytest
@@ -28,6 +33,7 @@ def prover():
     pk = gpu.ProvingKey(ctx, pkb, True)
     pk.precompute()
     p = Groth16Prover(ctx, pk, pk.vk_bytes())
+    p.pk_bytes = pkb
     yield p, opk
     import oracle_ctypes as O
     O.lib().oracle_pk_free(opk)
@@ -72,3 +78,55 @@ def test_l2_prove_matches_oracle(prover, batch_id, amount, consistent):
     from zelana_amd.l2block import public_inputs_fr
     c_ = l2_circuit_of(inp, w)
     assert PR.verify_with_oracle_vk(opk, 8, public_inputs_fr(c_), proof.a, proof.b, proof.c) == consistent
+
+
+def test_l2_gpu_witness_program_equals_host(prover):
+    """zkmi_wprog_run of the recorded L2BlockCircuit program == host z, for the
+    keygen shape and a wider one (new recipient, withdrawals), over batches
+    with other values than the recorded one."""
+    from test_l2_wprog import SHAPES, _batch
+    from zelana_amd import gpu, host_prover as H, wprog as W
+    p, _ = prover
+    for bal, tr, wd in SHAPES:
+        inp, w = _batch(5, bal, tr, wd)
+        _, z0, plan = H.l2_record(inp, w)
+        wp = W.WitnessProgram(p.ctx, plan)
+        dz = gpu.DeviceBuffer(p.ctx, plan.num_vars * 32)
+        try:
+            for bid, scale, rb in ((5, 1, 0), (77, 3, 9), (2 ** 63, 1000, 200)):
+                bal2 = {k: v * scale + bid % 7 for k, v in bal.items()}
+                tr2 = [(a, b, amt * scale + 1) for a, b, amt in tr]
+                wd2 = tuple((b, amt + scale) for b, amt in wd)
+                inp2, w2 = _batch(bid, bal2, tr2, wd2, rb) if bid != 5 else (inp, w)
+                _, zh = H.native_l2_block_circuit(inp2, w2)
+                wp.run(H.l2_witness_inputs(inp2, w2), dz)
+                zg = np.zeros_like(zh)
+                dz.download(zg)
+                bad = np.nonzero((zg != zh).any(1))[0]
+                assert bad.size == 0, f"GPU z differs at {bad[:8]} of {zh.shape[0]}"
+        finally:
+            wp.close()
+            dz.free()
+
+
+def test_native_prove_witness_program_path(prover):
+    """zp::Groth16Prover::prove (C++ drop-in): the first batch of the shape
+    records the program, later ones run it on the GPU; every proof equals the
+    Python mirror's (== the oracle's, test above) and the host-synthesis path's
+    (ZP_HOST_SYNTH=1)."""
+    import os
+    from zelana_amd.host_prover import NativeGroth16Prover
+    p, _ = prover
+    native = NativeGroth16Prover(p.pk_bytes, p.verifying_key, p.ctx.device)
+    try:
+        for batch_id, amount, consistent in [(0, 100, True), (42, 100, False), (41, 7, True), (9, 1000, False)]:
+            inp, w = _batch(batch_id, amount, consistent)
+            got, _ = native.prove(inp, w)
+            assert got == p.prove(inp, w).proof_bytes
+            os.environ["ZP_HOST_SYNTH"] = "1"
+            try:
+                assert native.prove(inp, w)[0] == got
+            finally:
+                del os.environ["ZP_HOST_SYNTH"]
+    finally:
+        native.close()

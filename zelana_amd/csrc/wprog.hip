@@ -14,6 +14,14 @@
 //   BITS64 z[out + i] = bit i of <a, z>, i < 64    (u64 range checks)
 //   PERM   z[out + 4 r + k] = (t_r^2, t_r^4, t_r^6, t_r^7), t_0 = <a, z> + c_0,
 //          t_r = t_{r-1}^7 + c_r                   (one MiMC permutation)
+// and, for L2BlockCircuit (prover/src/l2_circuit.rs:180-505, recorded by the
+// C++ synthesizer, zelana_amd/host/l2_circuit.cpp):
+//   BITS   z[out + i] = bit i of <a, z>, i < n     (to_non_unique_bits_le)
+//   NEQ    z[out] = (<a, z> != 0), z[out + 1] = <a, z>^-1 or 1   (is_neq)
+//   POSEIDON  one permutation of the width-3 sponge (l2_circuit.rs:68-83:
+//          x^5, 8 full + 56 partial rounds, Grain-LFSR constants): state in =
+//          three combinations, out = every S-box's x^2, x^4, x^5 in round
+//          order (round 0 skips constant elements, per the op's mask)
 // and each level is one launch; a batch uploads only its inputs.
 //
 // The program is latency-bound, not throughput-bound: its critical path is
@@ -41,8 +49,14 @@
 
 namespace zk {
 
-constexpr int WP_MUL = 1, WP_INV = 2, WP_BITS64 = 3, WP_PERM = 4;
+constexpr int WP_MUL = 1, WP_INV = 2, WP_BITS64 = 3, WP_PERM = 4, WP_BITS = 5, WP_NEQ = 6, WP_POSEIDON = 7;
 constexpr int MIMC_R = 91;
+// Poseidon (get_poseidon_config): constants at coefficient ids 3 r + i (ark)
+// and 192 + 3 i + j (MDS) of the program's table (zkmi.h)
+constexpr int POS_ROUNDS = 64, POS_FULL_HALF = 4, POS_NCONST = 201;
+__host__ __device__ constexpr uint32_t poseidon_trace_len(uint32_t mask) {
+  return 3 * ((mask & 1) + ((mask >> 1) & 1) + ((mask >> 2) & 1)) + 231;
+}
 
 // a * 2^-261 mod r for a < 2^261 with normalised limbs: Montgomery reduction
 // alone (a product with 1 without its 81 product mads)
@@ -234,6 +248,47 @@ __device__ __forceinline__ Fe sel(bool c, const Fe& a, const Fe& b) {
 // One level: op = lo + thread / 4, q = lane in its quad.  The four lanes of a
 // quad share an op, so a quad is either wholly active or wholly not (DPP
 // reads stay inside active quads).
+// One POSEIDON op on a quad: lane q < 3 holds state element q (Montgomery
+// form); each round adds its constant, S-boxes (all lanes in full rounds,
+// lane 0 in partial ones; the S-boxing lane stores x^2, x^4, x^5), then every
+// lane forms its MDS row from the three elements (DPP quad broadcasts).
+__device__ __forceinline__ void poseidon_quad(const Fe& in, uint32_t q, uint32_t out, uint32_t mask,
+                                              const Fe* __restrict__ pc, uint32_t* __restrict__ z) {
+  const uint32_t qq = q < 3 ? q : 2;
+  Fe s = mul<FrP>(in, fe_const<FrP>(FrP::R2));
+  const uint32_t m0 = 3 * __builtin_popcount(mask);  // trace values of round 0
+  for (int r = 0; r < POS_ROUNDS; r++) {
+    const Fe t = add<FrP>(s, pc[3 * r + qq]);
+    const bool full = r < POS_FULL_HALF || r >= POS_ROUNDS - POS_FULL_HALF;
+    Fe u = t;
+    if (full || q == 0) {
+      const Fe x2 = sqr_ilp(t), x4 = sqr_ilp(x2), x5 = mul_ilp(x4, t);
+      u = x5;
+      uint32_t at;
+      bool st = q < 3;
+      if (r == 0) {
+        st = st && ((mask >> q) & 1);
+        at = 3 * __builtin_popcount(mask & ((1u << q) - 1));
+      } else if (r < POS_FULL_HALF) {
+        at = m0 + 9 * (r - 1) + 3 * q;
+      } else if (!full) {
+        at = m0 + 27 + 3 * (r - POS_FULL_HALF);
+      } else {
+        at = m0 + 27 + 3 * (POS_ROUNDS - 2 * POS_FULL_HALF) + 9 * (r - (POS_ROUNDS - POS_FULL_HALF)) + 3 * q;
+      }
+      if (st) {
+        st_canon(z, out + at, redc_fr(x2));
+        st_canon(z, out + at + 1, redc_fr(x4));
+        st_canon(z, out + at + 2, redc_fr(x5));
+      }
+    }
+    const Fe b0 = quad_bcast<0>(u), b1 = quad_bcast<1>(u), b2 = quad_bcast<2>(u);
+    const Fe* row = pc + 3 * POS_ROUNDS + 3 * qq;
+    s = add<FrP>(add<FrP>(mul_ilp(row[0], b0), mul_ilp(row[1], b1)), mul_ilp(row[2], b2));
+  }
+}
+
+template <bool POS>
 __global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ ops, uint32_t lo, uint32_t hi,
                                                      const uint2* __restrict__ terms,
                                                      const uint32_t* __restrict__ coeff_m,
@@ -243,7 +298,10 @@ __global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ o
   // Round constants in LDS: a global load inside the round loop would make
   // every round wait (vmcnt) for the previous round's stores to land.
   __shared__ uint32_t rc_s[MIMC_R * 8];
+  __shared__ Fe pc_s[POS ? POS_NCONST : 1];  // Poseidon constants, unpacked Montgomery
   for (uint32_t i = threadIdx.x; i < MIMC_R * 8; i += blockDim.x) rc_s[i] = rc_m[i];
+  if constexpr (POS)
+    for (uint32_t i = threadIdx.x; i < POS_NCONST; i += blockDim.x) pc_s[i] = ld_canon(coeff_m, i);
   __syncthreads();
   // The program runs beside a proof whose MSM waves fill the same SIMDs:
   // top wave priority wins the VALU arbitration for this latency-critical
@@ -255,6 +313,16 @@ __global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ o
   const uint4 op = ops[op_i];
   const int kind = op.x & 0xFF;
   const uint32_t alen = (op.x >> 8) & 0xFFF, blen = op.x >> 20, out = op.y;
+  if constexpr (POS) {
+    if (kind == WP_POSEIDON) {
+      // lane q evaluates state combination q (stored contiguously at op.z)
+      const uint32_t l2 = op.w & 0xFFFF;
+      const uint32_t off = op.z + (q >= 1 ? alen : 0) + (q >= 2 ? blen : 0);
+      const uint32_t len = q == 0 ? alen : q == 1 ? blen : q == 2 ? l2 : 0;
+      poseidon_quad(eval_lc(terms, off, len, coeff_m, z), q, out, op.w >> 16, pc_s, z);
+      return;
+    }
+  }
   const Fe a = eval_lc(terms, op.z, alen, coeff_m, z);
   if (kind == WP_PERM) {
     const Fe r2 = fe_const<FrP>(FrP::R2);
@@ -275,10 +343,11 @@ __global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ o
     }
     return;
   }
-  if (kind == WP_BITS64) {
+  if (kind == WP_BITS64 || kind == WP_BITS) {
+    const uint32_t nbits = kind == WP_BITS ? op.w : 64;
     uint32_t w[8];
     pack(w, reduce<FrP>(a));
-    for (uint32_t i = q; i < 64; i += 4) {
+    for (uint32_t i = q; i < nbits; i += 4) {
       Fe b = fe_zero();
       b.v[0] = (w[i >> 5] >> (i & 31)) & 1;
       st_canon(z, out + i, b);
@@ -289,12 +358,28 @@ __global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ o
   if (kind == WP_MUL) {
     const Fe b = eval_lc(terms, op.w, blen, coeff_m, z);
     st_canon(z, out, mul<FrP>(mul<FrP>(a, fe_const<FrP>(FrP::R2)), b));
-  } else if (kind == WP_INV) {
+  } else if (kind == WP_INV || kind == WP_NEQ) {
     // r - 2 (Fermat); 0 stays 0
     const uint64_t e[4] = {0x43e1f593efffffffULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL,
                            0x30644e72e131a029ULL};
     const Fe am = mul<FrP>(a, fe_const<FrP>(FrP::R2));
-    st_canon(z, out, redc_fr(reduce<FrP>(pow<FrP>(am, e))));
+    Fe inv = redc_fr(reduce<FrP>(pow<FrP>(am, e)));
+    if (kind == WP_NEQ) {
+      // is_neq_const's witnesses: ne, then ne ? 1 / a : 1
+      const Fe ar = reduce<FrP>(a);
+      uint32_t nz = 0;
+#pragma unroll
+      for (int i = 0; i < NL; i++) nz |= ar.v[i];
+      Fe one_v = fe_zero();
+      one_v.v[0] = 1;
+      Fe ne = fe_zero();
+      ne.v[0] = nz != 0;
+      st_canon(z, out, ne);
+      if (!nz) inv = one_v;
+      st_canon(z, out + 1, inv);
+    } else {
+      st_canon(z, out, inv);
+    }
   }
 }
 
@@ -410,9 +495,19 @@ int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* d, zkmi_wprog** out)
   for (size_t i = 0; i < d->num_ops; i++) {
     const uint32_t* o = d->op + 4 * i;
     const uint32_t kind = o[0] & 0xFF, alen = (o[0] >> 8) & 0xFFF, blen = o[0] >> 20;
-    const uint64_t span = kind == WP_PERM ? 4 * MIMC_R : kind == WP_BITS64 ? 64 : 1;
-    if (kind < WP_MUL || kind > WP_PERM || o[1] + span > d->num_vars || (uint64_t)o[2] + alen > d->num_terms ||
-        (uint64_t)o[3] + blen > d->num_terms || (kind != WP_MUL && blen)) {
+    bool ok = kind >= WP_MUL && kind <= WP_POSEIDON;
+    uint64_t span = 1;
+    if (kind == WP_POSEIDON) {
+      const uint32_t l2 = o[3] & 0xFFFF, mask = o[3] >> 16;
+      span = poseidon_trace_len(mask);
+      ok = ok && mask >= 1 && mask <= 7 && l2 < 4096 && (uint64_t)o[2] + alen + blen + l2 <= d->num_terms &&
+           d->num_coeffs >= (size_t)POS_NCONST;
+    } else {
+      span = kind == WP_PERM ? 4 * MIMC_R : kind == WP_BITS64 ? 64 : kind == WP_BITS ? o[3] : kind == WP_NEQ ? 2 : 1;
+      ok = ok && (uint64_t)o[2] + alen <= d->num_terms && (kind == WP_MUL ? (uint64_t)o[3] + blen <= d->num_terms : !blen) &&
+           (kind != WP_BITS || (o[3] >= 1 && o[3] <= 256));
+    }
+    if (!ok || o[1] + span > d->num_vars) {
       set_error("zkmi_wprog_create: op %zu malformed", i);
       return ZKMI_EINVAL;
     }
@@ -545,8 +640,10 @@ int zkmi_wprog_run_many(zkmi_ctx* ctx, zkmi_wprog* p, size_t nb, const uint64_t*
     const uint32_t lo = p->level_start[l], hi = p->level_start[l + 1];
     if (hi == lo) continue;
     const size_t threads = (size_t)(hi - lo) * 4;
-    k_wprog_level<<<dim3((unsigned)((threads + 255) / 256), nby), 256, 0, st>>>(p->d_ops, lo, hi, p->d_terms,
-                                                                              p->d_coeff, p->d_rc, z, zs);
+    // permutations sort first in their level
+    auto kern = p->op_kinds[lo] == WP_POSEIDON ? k_wprog_level<true> : k_wprog_level<false>;
+    kern<<<dim3((unsigned)((threads + 255) / 256), nby), 256, 0, st>>>(p->d_ops, lo, hi, p->d_terms, p->d_coeff,
+                                                                       p->d_rc, z, zs);
   }
   if (p->num_perms) {
     const size_t nconv = (size_t)p->num_perms * (4 * MIMC_R - 1);

@@ -1,8 +1,10 @@
 // batch_prover.cpp — see batch_prover.h.
 #include "batch_prover.h"
 
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <fstream>
 #include <iterator>
@@ -81,6 +83,7 @@ std::unique_ptr<Groth16Prover> Groth16Prover::from_files(const std::string& pk_p
 }
 
 Groth16Prover::~Groth16Prover() {
+  shapes_.clear();  // before the context
   if (pk_) zkmi_pk_destroy(pk_);
   if (ctx_) zkmi_ctx_destroy(ctx_);
 }
@@ -103,14 +106,22 @@ L2BlockCircuit Groth16Prover::circuit_of(const BatchPublicInputs& in, const Batc
   return c;
 }
 
-BatchProof Groth16Prover::prove(const BatchPublicInputs& inputs, const BatchWitness& witness) const {
-  const auto start = std::chrono::steady_clock::now();
-  StdRng rng = StdRng::seed_from_u64(inputs.batch_id);  // prover.rs:354
-  const R1CSMatrices m = circuit_of(inputs, witness).synthesize();
-  // Groth16::prove: r = Fr::rand, then s = Fr::rand
-  uint64_t r[4], s[4];
-  rng.fr_rand().to_canon(r);
-  rng.fr_rand().to_canon(s);
+// One circuit shape's resident state (see batch_prover.h).
+struct Groth16Prover::Shape {
+  std::string key;
+  zkmi_ctx* ctx = nullptr;
+  zkmi_r1cs_dev* cs = nullptr;
+  zkmi_wprog* prog = nullptr;
+  void* d_z = nullptr;
+  ~Shape() {
+    if (prog) zkmi_wprog_destroy(prog);
+    if (cs) zkmi_r1cs_destroy(cs);
+    if (d_z) zkmi_dev_free(ctx, d_z);
+  }
+};
+
+namespace {
+zkmi_r1cs r1cs_view(const R1CSMatrices& m) {
   zkmi_r1cs cs;
   cs.num_constraints = m.num_constraints;
   cs.num_instance = m.num_instance;
@@ -123,6 +134,82 @@ BatchProof Groth16Prover::prove(const BatchPublicInputs& inputs, const BatchWitn
     *cols[t] = m.col[t].data();
     *vals[t] = m.val[t].data();
   }
+  return cs;
+}
+bool host_synthesis_forced() {
+  const char* e = getenv("ZP_HOST_SYNTH");  // A/B switch: the round-2 per-call host synthesis
+  return e && e[0] == '1';
+}
+}  // namespace
+
+BatchProof Groth16Prover::prove(const BatchPublicInputs& inputs, const BatchWitness& witness) const {
+  const auto start = std::chrono::steady_clock::now();
+  const L2BlockCircuit circuit = circuit_of(inputs, witness);
+  if (host_synthesis_forced()) return prove_host(inputs, circuit);
+  StdRng rng = StdRng::seed_from_u64(inputs.batch_id);  // prover.rs:354
+  // Groth16::prove: r = Fr::rand, then s = Fr::rand
+  uint64_t r[4], s[4];
+  rng.fr_rand().to_canon(r);
+  rng.fr_rand().to_canon(s);
+  const std::string key = circuit.shape_key();  // throws synthesize's errors
+  uint64_t a[8], b[16], c[8];
+  {
+    std::lock_guard<std::mutex> lock(gpu_mu_);
+    size_t hit = shapes_.size();
+    for (size_t i = 0; i < shapes_.size(); i++)
+      if (shapes_[i]->key == key) hit = i;
+    std::vector<uint64_t> in;
+    if (hit == shapes_.size()) {
+      // first batch of this shape: synthesize once, recording its program
+      L2WitnessProgram prog;
+      const R1CSMatrices m = circuit.synthesize(nullptr, &prog);
+      std::unique_ptr<Shape> sh(new Shape());
+      sh->key = key;
+      sh->ctx = ctx_;
+      const zkmi_r1cs view = r1cs_view(m);
+      check(zkmi_r1cs_create(ctx_, &view, &sh->cs), "Failed to upload the circuit");
+      zkmi_wprog_desc d;
+      d.num_vars = prog.num_vars;
+      d.num_inputs = prog.input_var.size();
+      d.input_var = prog.input_var.data();
+      d.num_ops = prog.op.size() / 4;
+      d.op = prog.op.data();
+      d.num_terms = prog.term.size() / 2;
+      d.term = prog.term.data();
+      d.num_coeffs = prog.coeff.size() / 4;
+      d.coeff = prog.coeff.data();
+      d.num_levels = prog.num_levels();
+      d.level_start = prog.level_start.data();
+      check(zkmi_wprog_create(ctx_, &d, &sh->prog), "Failed to load the witness program");
+      check(zkmi_dev_alloc(ctx_, prog.num_vars * 32, &sh->d_z), "Failed to allocate the assignment");
+      in = std::move(prog.template_inputs);
+      if (shapes_.size() == kMaxShapes) shapes_.pop_back();
+      shapes_.insert(shapes_.begin(), std::move(sh));
+    } else {
+      in = circuit.witness_inputs();
+      std::rotate(shapes_.begin(), shapes_.begin() + hit, shapes_.begin() + hit + 1);
+    }
+    const Shape& sh = *shapes_.front();
+    check(zkmi_wprog_run(ctx_, sh.prog, in.data(), sh.d_z, 0), "Witness generation failed");
+    if (zkmi_groth16_prove_resident(ctx_, pk_, sh.cs, sh.d_z, r, s, a, b, c) != 0) fail("Proving failed");
+  }
+  BatchProof p;
+  p.public_inputs = inputs;
+  p.proof_bytes = proof_to_solana_bytes(a, b, c);
+  p.proving_time_ms =
+      (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - start).count();
+  return p;
+}
+
+// Round-2 path (ZP_HOST_SYNTH=1): full host synthesis per call, R1CS and z uploaded
+BatchProof Groth16Prover::prove_host(const BatchPublicInputs& inputs, const L2BlockCircuit& circuit) const {
+  const auto start = std::chrono::steady_clock::now();
+  StdRng rng = StdRng::seed_from_u64(inputs.batch_id);
+  const R1CSMatrices m = circuit.synthesize();
+  uint64_t r[4], s[4];
+  rng.fr_rand().to_canon(r);
+  rng.fr_rand().to_canon(s);
+  const zkmi_r1cs cs = r1cs_view(m);
   uint64_t a[8], b[16], c[8];
   {
     std::lock_guard<std::mutex> lock(gpu_mu_);  // synthesis above runs unlocked, in parallel

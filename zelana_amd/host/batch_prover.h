@@ -11,8 +11,11 @@
 //                          proof_to_solana_bytes }                 :252-447
 //
 // Every field / curve / polynomial operation of Groth16Prover::prove runs on
-// the MI355X; the host does L2BlockCircuit synthesis (l2_circuit.h) and the
-// StdRng draws.
+// the MI355X, the witness included: the first batch of a circuit shape is
+// synthesized on the host (l2_circuit.h), which records the shape's witness
+// program and uploads its R1CS; every later batch of that shape only extracts
+// its free inputs on the host and runs the program on the GPU (zkmi_wprog_run)
+// straight into the resident prove.  The host keeps the StdRng draws.
 #pragma once
 #include <stdint.h>
 
@@ -130,6 +133,12 @@ class Groth16Prover : public BatchProver {
   // BatchProver is shared (Arc<dyn BatchProver>: Send + Sync) but a zkmi
   // context serves one call at a time (zkmi.h): prove() serialises on it
   mutable std::mutex gpu_mu_;
+  // per circuit shape: witness program + resident R1CS + z buffer (most
+  // recently used first, at most kMaxShapes; guarded by gpu_mu_)
+  struct Shape;
+  static constexpr size_t kMaxShapes = 8;
+  mutable std::vector<std::unique_ptr<Shape>> shapes_;
+  BatchProof prove_host(const BatchPublicInputs& inputs, const L2BlockCircuit& c) const;
 };
 
 // BLAKE3 compute_batch_hash over the transactions (prover.rs:525-558)

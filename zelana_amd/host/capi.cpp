@@ -89,6 +89,74 @@ int zp_l2_synthesize(const uint8_t* inputs, const uint8_t* tr, size_t nt, const 
     return guard(e);
   }
 }
+// The same synthesis, also recording the witness program of the circuit's
+// shape: *r1cs_out as zp_l2_synthesize, *prog_out a zp_wprog_* handle
+int zp_l2_record(const uint8_t* inputs, const uint8_t* tr, size_t nt, const uint8_t* wd, size_t nw, const uint8_t* ac,
+                 size_t na, void** r1cs_out, void** prog_out) {
+  try {
+    L2BlockCircuit c = Groth16Prover::circuit_of(parse_inputs(inputs), parse_witness(tr, nt, wd, nw, ac, na));
+    std::unique_ptr<L2WitnessProgram> p(new L2WitnessProgram());
+    *r1cs_out = new R1CSMatrices(c.synthesize(nullptr, p.get()));
+    *prog_out = p.release();
+    return 0;
+  } catch (const std::exception& e) {
+    return guard(e);
+  }
+}
+// a batch's free inputs (num_inputs x 4 u64; call with out = NULL for the count)
+int zp_l2_witness_inputs(const uint8_t* inputs, const uint8_t* tr, size_t nt, const uint8_t* wd, size_t nw,
+                         const uint8_t* ac, size_t na, uint64_t* out, size_t* n_inputs) {
+  try {
+    L2BlockCircuit c = Groth16Prover::circuit_of(parse_inputs(inputs), parse_witness(tr, nt, wd, nw, ac, na));
+    std::vector<uint64_t> v = c.witness_inputs();
+    *n_inputs = v.size() / 4;
+    if (out) memcpy(out, v.data(), v.size() * 8);
+    return 0;
+  } catch (const std::exception& e) {
+    return guard(e);
+  }
+}
+int zp_l2_shape_key(const uint8_t* inputs, const uint8_t* tr, size_t nt, const uint8_t* wd, size_t nw,
+                    const uint8_t* ac, size_t na, char* out, size_t cap) {
+  try {
+    L2BlockCircuit c = Groth16Prover::circuit_of(parse_inputs(inputs), parse_witness(tr, nt, wd, nw, ac, na));
+    const std::string k = c.shape_key();
+    if (k.size() + 1 > cap) throw std::runtime_error("shape key buffer too small");
+    memcpy(out, k.c_str(), k.size() + 1);
+    return 0;
+  } catch (const std::exception& e) {
+    return guard(e);
+  }
+}
+// sizes: num_vars, num_inputs, num_ops, num_terms, num_coeffs, num_levels
+void zp_wprog_sizes(const void* h, uint64_t out[6]) {
+  const L2WitnessProgram* p = (const L2WitnessProgram*)h;
+  out[0] = p->num_vars, out[1] = p->input_var.size(), out[2] = p->op.size() / 4, out[3] = p->term.size() / 2;
+  out[4] = p->coeff.size() / 4, out[5] = p->num_levels();
+}
+void zp_wprog_copy(const void* h, uint32_t* input_var, uint32_t* op, uint32_t* term, uint64_t* coeff,
+                   uint32_t* level_start, uint64_t* template_inputs) {
+  const L2WitnessProgram* p = (const L2WitnessProgram*)h;
+  memcpy(input_var, p->input_var.data(), p->input_var.size() * 4);
+  memcpy(op, p->op.data(), p->op.size() * 4);
+  memcpy(term, p->term.data(), p->term.size() * 4);
+  memcpy(coeff, p->coeff.data(), p->coeff.size() * 8);
+  memcpy(level_start, p->level_start.data(), p->level_start.size() * 4);
+  memcpy(template_inputs, p->template_inputs.data(), p->template_inputs.size() * 8);
+}
+int zp_wprog_interpret(const void* h, const uint64_t* inputs, uint64_t* z_out) {
+  try {
+    const L2WitnessProgram* p = (const L2WitnessProgram*)h;
+    std::vector<uint64_t> in(inputs, inputs + 4 * p->input_var.size());
+    std::vector<uint64_t> z = p->interpret(in);
+    memcpy(z_out, z.data(), z.size() * 8);
+    return 0;
+  } catch (const std::exception& e) {
+    return guard(e);
+  }
+}
+void zp_wprog_free(void* h) { delete (L2WitnessProgram*)h; }
+
 // sizes: m, num_instance, num_witness, nnz(a), nnz(b), nnz(c), satisfied
 void zp_r1cs_sizes(const void* h, uint64_t out[7]) {
   const R1CSMatrices* m = (const R1CSMatrices*)h;

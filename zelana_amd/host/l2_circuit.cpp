@@ -3,6 +3,8 @@
 // arkworks 0.5 gadgets) so the C++ host mirror needs no Python.
 #include "l2_circuit.h"
 
+#include <algorithm>
+#include <set>
 #include <stdexcept>
 
 namespace zp {
@@ -130,16 +132,42 @@ LC lc_scale(const LC& a, const Fr& c) {
   return o;
 }
 
+// witness-program op kinds (zkmi.h)
+constexpr uint32_t WP_MUL = 1, WP_BITS = 5, WP_NEQ = 6, WP_POSEIDON = 7;
+
 struct CS {
   std::vector<Fr> inst{Fr::one()}, wit;
   std::vector<std::array<LC, 3>> rows;
+  // Witness-program recording: the free inputs (symbols, allocation order)
+  // and one op per computed witness group.  `mute` > 0 inside a gadget that
+  // records itself as one op (a permutation, a bit decomposition).
+  struct Rec {
+    uint32_t kind;
+    uint64_t out;  // first output symbol
+    std::vector<LC> lcs;
+    uint32_t aux;  // BITS: bit count; POSEIDON: round-0 variable mask
+  };
+  bool record = false;
+  int mute = 0;
+  std::vector<Rec> ops;
+  std::vector<uint64_t> in_syms{0};  // One
+  void op(uint32_t kind, uint64_t out, std::vector<LC> lcs, uint32_t aux = 0) {
+    if (record && !mute) ops.push_back({kind, out, std::move(lcs), aux});
+  }
+  uint64_t next_witness() const { return kWit + wit.size(); }
   LC new_input(const Fr& v) {
     inst.push_back(v);
+    in_syms.push_back(inst.size() - 1);
     return LC{{inst.size() - 1, Fr::one()}};
   }
   LC new_witness(const Fr& v) {
     wit.push_back(v);
     return LC{{kWit + wit.size() - 1, Fr::one()}};
+  }
+  // a witness taken from the batch's data (a free input of the program)
+  LC new_data(const Fr& v) {
+    in_syms.push_back(next_witness());
+    return new_witness(v);
   }
   void enforce(const LC& a, const LC& b, const LC& c) { rows.push_back({a, b, c}); }
 };
@@ -155,6 +183,7 @@ struct FpVar {
   static FpVar constant(CS* cs, const Fr& v) { return FpVar{cs, true, {}, v}; }
   static FpVar input(CS* cs, const Fr& v) { return FpVar{cs, false, cs->new_input(v), v}; }
   static FpVar witness(CS* cs, const Fr& v) { return FpVar{cs, false, cs->new_witness(v), v}; }
+  static FpVar data(CS* cs, const Fr& v) { return FpVar{cs, false, cs->new_data(v), v}; }
   LC term() const { return is_const ? one_lc(v) : lc; }
   FpVar operator+(const FpVar& o) const {
     if (is_const && o.is_const) return constant(cs, v + o.v);
@@ -173,12 +202,14 @@ struct FpVar {
     if (is_const) return o.scale(v);
     if (o.is_const) return scale(o.v);
     FpVar p = witness(cs, v * o.v);
+    cs->op(WP_MUL, p.lc[0].first, {lc, o.lc});
     cs->enforce(lc, o.lc, p.lc);
     return p;
   }
   FpVar square() const {
     if (is_const) return constant(cs, v * v);
     FpVar p = witness(cs, v * v);
+    cs->op(WP_MUL, p.lc[0].first, {lc, lc});
     cs->enforce(lc, lc, p.lc);
     return p;
   }
@@ -223,6 +254,7 @@ struct Boolean {
     if (is_const) return v ? o : *this;
     if (o.is_const) return o.v ? *this : o;
     Boolean r{cs, false, cs->new_witness(Fr::from_u64(v && o.v)), v && o.v};
+    cs->op(WP_MUL, r.lc[0].first, {lc, o.lc});
     cs->enforce(lc, o.lc, r.lc);
     return r;
   }
@@ -243,6 +275,7 @@ Boolean is_neq_const(const FpVar& x, const Fr& c) {
   Boolean nb{cs, false, cs->new_witness(Fr::from_u64(ne)), ne};
   FpVar mult = FpVar::witness(cs, ne ? d.inverse() : Fr::one());
   const LC diff = lc_add(one_lc(c), x.term(), true);
+  cs->op(WP_NEQ, nb.lc[0].first, {diff});  // nb, then mult
   cs->enforce(diff, mult.lc, nb.lc);
   cs->enforce(diff, nb.negate().term(), LC{});
   return nb;
@@ -303,7 +336,10 @@ void enforce_le(const std::vector<Boolean>& bits, const uint64_t el[4]) {
 std::vector<Boolean> to_non_unique_bits_le(const FpVar& x) {
   CS* cs = x.cs;
   std::vector<Boolean> bits;
+  cs->op(WP_BITS, cs->next_witness(), {x.term()}, kModulusBits);
+  cs->mute++;
   for (int i = 0; i < kModulusBits; i++) bits.push_back(Boolean::witness(cs, x.v.bit(i)));
+  cs->mute--;
   LC packed;
   Fr coeff = Fr::one();
   for (const Boolean& b : bits) {
@@ -341,6 +377,15 @@ struct Sponge {
   }
   void permute() {
     const int half = p.full / 2;
+    // one POSEIDON op: the three state combinations in, the S-box trace
+    // (x^2, x^4, x^5 per S-box, round order) out; round 0 skips constant
+    // elements (their powers are constants, no witnesses)
+    uint32_t mask = 0;
+    for (int i = 0; i < 3; i++)
+      if (!st[i].is_const) mask |= 1u << i;
+    const uint64_t first = cs->next_witness();
+    if (mask) cs->op(WP_POSEIDON, first, {st[0].term(), st[1].term(), st[2].term()}, mask);
+    cs->mute++;
     for (int rnd = 0; rnd < p.full + p.partial; rnd++) {
       for (int i = 0; i < 3; i++) st[i] = st[i] + p.ark[rnd][i];
       if (rnd < half || rnd >= half + p.partial) {
@@ -356,6 +401,10 @@ struct Sponge {
       }
       st = nw;
     }
+    cs->mute--;
+    const uint64_t trace = cs->next_witness() - first;
+    if (trace != (mask ? 3 * (uint64_t)__builtin_popcount(mask) + 231 : 0))
+      throw std::logic_error("Poseidon trace length differs from the POSEIDON op's");
   }
   void absorb_internal(int start, std::vector<FpVar> el) {
     for (;;) {
@@ -429,9 +478,14 @@ L2BlockCircuit L2BlockCircuit::dummy() {
   return c;
 }
 
-R1CSMatrices L2BlockCircuit::synthesize(std::map<std::string, Fr>* computed) const {
+namespace {
+void build_program(const CS& cs, L2WitnessProgram& P);
+}  // namespace
+
+R1CSMatrices L2BlockCircuit::synthesize(std::map<std::string, Fr>* computed, L2WitnessProgram* prog) const {
   CS cs;
   CS* C = &cs;
+  cs.record = prog != nullptr;
   auto sponge = [&](const std::vector<FpVar>& el) {
     Sponge sp(C);
     sp.absorb(el);
@@ -447,10 +501,10 @@ R1CSMatrices L2BlockCircuit::synthesize(std::map<std::string, Fr>* computed) con
   std::map<std::string, Fr> out;
 
   std::map<Bytes32, FpVar> accounts;
-  for (const auto& kv : initial_accounts) accounts[kv.first] = FpVar::witness(C, Fr::from_u64(kv.second));
+  for (const auto& kv : initial_accounts) accounts[kv.first] = FpVar::data(C, Fr::from_u64(kv.second));
   std::map<Bytes32, FpVar> current = accounts;
   for (const auto& tx : transactions) {
-    FpVar amount = FpVar::witness(C, Fr::from_u64(tx.amount));
+    FpVar amount = FpVar::data(C, Fr::from_u64(tx.amount));
     auto it = current.find(tx.sender_pk);
     if (it == current.end()) throw std::runtime_error("SynthesisError::AssignmentMissing: sender not in initial_accounts");
     FpVar sender = it->second;
@@ -464,11 +518,11 @@ R1CSMatrices L2BlockCircuit::synthesize(std::map<std::string, Fr>* computed) con
   auto fold_accounts = [&](const std::map<Bytes32, FpVar>& accts) {
     FpVar st = sponge({ds, bid});
     for (const auto& kv : accts) {
-      FpVar pk = FpVar::witness(C, fr_le(kv.first));
+      FpVar pk = FpVar::data(C, fr_le(kv.first));
       FpVar leaf = sponge({pk, kv.second});
       st = sponge({st, leaf});
     }
-    FpVar count = FpVar::witness(C, Fr::from_u64(accts.size()));
+    FpVar count = FpVar::data(C, Fr::from_u64(accts.size()));
     return sponge({st, count});
   };
   FpVar computed_post = fold_accounts(current);
@@ -477,7 +531,7 @@ R1CSMatrices L2BlockCircuit::synthesize(std::map<std::string, Fr>* computed) con
 
   FpVar sh = sponge({pre_shielded});
   for (const auto& cm : shielded_commitments) {
-    FpVar cmv = FpVar::witness(C, fr_le(cm));
+    FpVar cmv = FpVar::data(C, fr_le(cm));
     sh = sponge({sh, cmv});
   }
   if (shielded_commitments.empty()) {
@@ -490,25 +544,25 @@ R1CSMatrices L2BlockCircuit::synthesize(std::map<std::string, Fr>* computed) con
 
   FpVar wd = sponge({FpVar::constant(C, fr_str("zelana:withdrawals:v1"))});
   for (const auto& w : withdrawals) {
-    FpVar rcp = FpVar::witness(C, fr_le(w.recipient));
-    FpVar amt = FpVar::witness(C, Fr::from_u64(w.amount));
+    FpVar rcp = FpVar::data(C, fr_le(w.recipient));
+    FpVar amt = FpVar::data(C, Fr::from_u64(w.amount));
     FpVar leaf = sponge({rcp, amt});
     wd = sponge({wd, leaf});
   }
-  FpVar wd_count = FpVar::witness(C, Fr::from_u64(withdrawals.size()));
+  FpVar wd_count = FpVar::data(C, Fr::from_u64(withdrawals.size()));
   FpVar computed_wd = sponge({wd, wd_count});
   out["withdrawal_root"] = computed_wd.v;
   computed_wd.enforce_equal(wd_root);
 
   FpVar bst = sponge({FpVar::constant(C, fr_str("zelana:batch-hash:v1")), bid});
   for (const auto& tx : transactions) {
-    FpVar s = FpVar::witness(C, fr_le(tx.sender_pk));
-    FpVar r = FpVar::witness(C, fr_le(tx.recipient_pk));
-    FpVar a = FpVar::witness(C, Fr::from_u64(tx.amount));
+    FpVar s = FpVar::data(C, fr_le(tx.sender_pk));
+    FpVar r = FpVar::data(C, fr_le(tx.recipient_pk));
+    FpVar a = FpVar::data(C, Fr::from_u64(tx.amount));
     FpVar txh = sponge({s, r, a});
     bst = sponge({bst, txh});
   }
-  FpVar tx_count = FpVar::witness(C, Fr::from_u64(transactions.size()));
+  FpVar tx_count = FpVar::data(C, Fr::from_u64(transactions.size()));
   FpVar computed_bh = sponge({bst, tx_count});
   out["batch_hash"] = computed_bh.v;
   computed_bh.enforce_equal(bh);
@@ -547,7 +601,263 @@ R1CSMatrices L2BlockCircuit::synthesize(std::map<std::string, Fr>* computed) con
     v.to_canon(c);
     M.z.insert(M.z.end(), c, c + 4);
   }
+  if (prog) build_program(cs, *prog);
   return M;
+}
+
+// ------------------------------------------------------- witness programs
+namespace {
+
+uint64_t op_span(uint32_t kind, uint32_t aux) {
+  switch (kind) {
+    case WP_MUL: return 1;
+    case WP_BITS: return aux;
+    case WP_NEQ: return 2;
+    default: return 3 * (uint64_t)__builtin_popcount(aux) + 231;  // POSEIDON
+  }
+}
+
+// The recorded ops scheduled into launch levels, as zelana_amd/wprog.py's
+// Plan does for zelana_batch: a permutation costs ~1000x a MUL, so the key is
+// (permutation stage, cheap sub-level) and every permutation runs at its
+// chain's permutation depth.
+void build_program(const CS& cs, L2WitnessProgram& P) {
+  const uint64_t ni = cs.inst.size(), nv = ni + cs.wit.size();
+  if (nv >= (1ULL << 31)) throw std::runtime_error("witness program: too many variables");
+  auto zidx = [&](uint64_t sym) { return (uint32_t)(sym >= kWit ? ni + (sym - kWit) : sym); };
+  P = L2WitnessProgram();
+  P.num_vars = nv;
+  P.num_instance = ni;
+  std::map<std::array<uint64_t, 4>, uint32_t> cid;
+  auto push_coeff = [&](const Fr& c, bool dedupe) {
+    std::array<uint64_t, 4> k;
+    c.to_canon(k.data());
+    if (dedupe) {
+      auto it = cid.find(k);
+      if (it != cid.end()) return it->second;
+    }
+    const uint32_t id = (uint32_t)(P.coeff.size() / 4);
+    cid.emplace(k, id);
+    P.coeff.insert(P.coeff.end(), k.begin(), k.end());
+    return id;
+  };
+  const PoseidonParams& pp = poseidon_params();  // ids 3r + i, then 192 + 3i + j (zkmi.h)
+  for (int r = 0; r < 64; r++)
+    for (int i = 0; i < 3; i++) push_coeff(pp.ark[r][i], false);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) push_coeff(pp.mds[i][j], false);
+
+  std::vector<uint8_t> produced(nv, 0);
+  for (uint64_t sym : cs.in_syms) {
+    const uint32_t v = zidx(sym);
+    if (produced[v]) throw std::logic_error("witness program: input allocated twice");
+    produced[v] = 1;
+    P.input_var.push_back(v);
+    const Fr& val = sym >= kWit ? cs.wit[sym - kWit] : cs.inst[sym];
+    uint64_t c[4];
+    val.to_canon(c);
+    P.template_inputs.insert(P.template_inputs.end(), c, c + 4);
+  }
+  constexpr uint64_t BIG = 0xFFFFFFFFULL;
+  std::vector<uint32_t> pstage(nv, 0), sub(nv, 0);
+  struct Sched {
+    uint64_t key;
+    bool pos;
+    size_t i;
+  };
+  std::vector<Sched> order;
+  for (size_t i = 0; i < cs.ops.size(); i++) {
+    const CS::Rec& o = cs.ops[i];
+    uint32_t s_in = 0;
+    for (const LC& lc : o.lcs)
+      for (const auto& t : lc)
+        if (!t.second.is_zero() && t.first) s_in = std::max(s_in, pstage[zidx(t.first)]);
+    const uint64_t span = op_span(o.kind, o.aux), out = zidx(o.out);
+    if (out + span > nv) throw std::logic_error("witness program: op output outside z");
+    uint32_t st, sl;
+    uint64_t key;
+    if (o.kind == WP_POSEIDON) {
+      st = s_in + 1, sl = 0;
+      key = ((uint64_t)s_in << 32) | BIG;
+    } else {
+      sl = 0;
+      for (const LC& lc : o.lcs)
+        for (const auto& t : lc)
+          if (!t.second.is_zero() && t.first && pstage[zidx(t.first)] == s_in) sl = std::max(sl, sub[zidx(t.first)]);
+      st = s_in, sl += 1;
+      key = ((uint64_t)s_in << 32) | sl;
+    }
+    for (uint64_t v = out; v < out + span; v++) {
+      if (produced[v]) throw std::logic_error("witness program: variable written twice");
+      produced[v] = 1;
+      pstage[v] = st;
+      sub[v] = sl;
+    }
+    order.push_back({key, o.kind == WP_POSEIDON, i});
+  }
+  for (uint64_t v = 0; v < nv; v++)
+    if (!produced[v]) throw std::logic_error("witness program: variable neither input nor op output");
+  // within a level: permutations first (the quads of one wave share a kind)
+  std::stable_sort(order.begin(), order.end(), [](const Sched& a, const Sched& b) {
+    return a.key != b.key ? a.key < b.key : (a.pos && !b.pos);
+  });
+  auto emit = [&](const LC& lc) {
+    uint32_t n = 0;
+    for (const auto& t : lc) {
+      if (t.second.is_zero()) continue;
+      P.term.push_back(zidx(t.first));
+      P.term.push_back(push_coeff(t.second, true));
+      n++;
+    }
+    if (n >= 4096) throw std::runtime_error("witness program: linear combination over 4095 terms");
+    return n;
+  };
+  for (size_t k = 0; k < order.size(); k++) {
+    if (k == 0 || order[k].key != order[k - 1].key) P.level_start.push_back((uint32_t)k);
+    const CS::Rec& o = cs.ops[order[k].i];
+    const uint32_t aoff = (uint32_t)(P.term.size() / 2);
+    uint32_t w[4] = {o.kind, zidx(o.out), aoff, 0};
+    if (o.kind == WP_MUL) {
+      const uint32_t la = emit(o.lcs[0]);
+      w[3] = (uint32_t)(P.term.size() / 2);
+      const uint32_t lb = emit(o.lcs[1]);
+      w[0] |= la << 8 | lb << 20;
+    } else if (o.kind == WP_POSEIDON) {
+      const uint32_t l0 = emit(o.lcs[0]), l1 = emit(o.lcs[1]), l2 = emit(o.lcs[2]);
+      w[0] |= l0 << 8 | l1 << 20;
+      w[3] = l2 | o.aux << 16;
+    } else {
+      w[0] |= emit(o.lcs[0]) << 8;
+      w[3] = o.kind == WP_BITS ? o.aux : 0;
+    }
+    P.op.insert(P.op.end(), w, w + 4);
+  }
+  P.level_start.push_back((uint32_t)order.size());
+}
+
+}  // namespace
+
+std::vector<uint64_t> L2WitnessProgram::interpret(const std::vector<uint64_t>& inputs) const {
+  if (inputs.size() != input_var.size() * 4) throw std::invalid_argument("witness program: input count");
+  std::vector<Fr> z(num_vars), co(coeff.size() / 4);
+  for (size_t k = 0; k < input_var.size(); k++) z[input_var[k]] = Fr::from_canon(&inputs[4 * k]);
+  for (size_t k = 0; k < co.size(); k++) co[k] = Fr::from_canon(&coeff[4 * k]);
+  auto ev = [&](uint32_t off, uint32_t n) {
+    Fr s;
+    for (uint32_t k = off; k < off + n; k++) s = s + co[term[2 * k + 1]] * z[term[2 * k]];
+    return s;
+  };
+  for (size_t i = 0; i < op.size() / 4; i++) {
+    const uint32_t* o = &op[4 * i];
+    const uint32_t kind = o[0] & 0xFF, la = (o[0] >> 8) & 0xFFF, lb = o[0] >> 20, out = o[1];
+    if (kind == WP_MUL) {
+      z[out] = ev(o[2], la) * ev(o[3], lb);
+    } else if (kind == WP_BITS) {
+      const Fr a = ev(o[2], la);
+      for (uint32_t b = 0; b < o[3]; b++) z[out + b] = Fr::from_u64(a.bit((int)b));
+    } else if (kind == WP_NEQ) {
+      const Fr a = ev(o[2], la);
+      z[out] = Fr::from_u64(!a.is_zero());
+      z[out + 1] = a.is_zero() ? Fr::one() : a.inverse();
+    } else if (kind == WP_POSEIDON) {
+      const uint32_t l2 = o[3] & 0xFFFF, mask = o[3] >> 16;
+      Fr st[3] = {ev(o[2], la), ev(o[2] + la, lb), ev(o[2] + la + lb, l2)};
+      uint32_t t = out;
+      for (int r = 0; r < 64; r++) {
+        for (int j = 0; j < 3; j++) st[j] = st[j] + co[3 * r + j];
+        const bool full = r < 4 || r >= 60;
+        for (int j = 0; j < (full ? 3 : 1); j++) {
+          const Fr x2 = st[j] * st[j], x4 = x2 * x2, x5 = x4 * st[j];
+          if (r > 0 || ((mask >> j) & 1)) {
+            z[t++] = x2;
+            z[t++] = x4;
+            z[t++] = x5;
+          }
+          st[j] = x5;
+        }
+        Fr nw[3];
+        for (int j = 0; j < 3; j++) nw[j] = co[192 + 3 * j] * st[0] + co[192 + 3 * j + 1] * st[1] + co[192 + 3 * j + 2] * st[2];
+        for (int j = 0; j < 3; j++) st[j] = nw[j];
+      }
+    } else {
+      throw std::invalid_argument("witness program: unknown op kind");
+    }
+  }
+  std::vector<uint64_t> zc(4 * num_vars);
+  for (uint64_t v = 0; v < num_vars; v++) z[v].to_canon(&zc[4 * v]);
+  return zc;
+}
+
+std::string L2BlockCircuit::shape_key() const {
+  std::map<Bytes32, uint32_t> rank;
+  for (const auto& kv : initial_accounts) rank[kv.first] = 0;
+  for (const auto& tx : transactions) rank[tx.sender_pk] = rank[tx.recipient_pk] = 0;
+  uint32_t k = 0;
+  for (auto& kv : rank) kv.second = k++;
+  std::string s = "t" + std::to_string(transactions.size()) + "a" + std::to_string(initial_accounts.size()) + "k" +
+                  std::to_string(rank.size()) + "s" + std::to_string(shielded_commitments.size()) + "w" +
+                  std::to_string(withdrawals.size()) + ":";
+  std::set<Bytes32> cur;
+  for (const auto& kv : initial_accounts) {
+    cur.insert(kv.first);
+    s += std::to_string(rank[kv.first]) + ",";
+  }
+  s += ":";
+  for (const auto& tx : transactions) {
+    if (!cur.count(tx.sender_pk))
+      throw std::runtime_error("SynthesisError::AssignmentMissing: sender not in initial_accounts");
+    s += std::to_string(rank[tx.sender_pk]) + ">" + std::to_string(rank[tx.recipient_pk]) +
+         (cur.count(tx.recipient_pk) ? "," : "+,");
+    cur.insert(tx.recipient_pk);
+  }
+  return s;
+}
+
+std::vector<uint64_t> L2BlockCircuit::witness_inputs() const {
+  // synthesize()'s allocation order of FpVar::input / FpVar::data
+  std::vector<uint64_t> out;
+  auto put = [&](const Fr& v) {
+    uint64_t c[4];
+    v.to_canon(c);
+    out.insert(out.end(), c, c + 4);
+  };
+  put(Fr::one());
+  for (const Bytes32* r : {&pre_state_root, &post_state_root, &pre_shielded_root, &post_shielded_root,
+                           &withdrawal_root, &batch_hash})
+    put(fr_le(*r));
+  put(Fr::from_u64(batch_id));
+  std::set<Bytes32> current;
+  for (const auto& kv : initial_accounts) {
+    put(Fr::from_u64(kv.second));
+    current.insert(kv.first);
+  }
+  for (const auto& tx : transactions) {
+    put(Fr::from_u64(tx.amount));
+    if (!current.count(tx.sender_pk))
+      throw std::runtime_error("SynthesisError::AssignmentMissing: sender not in initial_accounts");
+    current.insert(tx.recipient_pk);
+  }
+  auto fold = [&](const std::set<Bytes32>& keys) {
+    for (const Bytes32& pk : keys) put(fr_le(pk));
+    put(Fr::from_u64(keys.size()));
+  };
+  fold(current);
+  for (const auto& cm : shielded_commitments) put(fr_le(cm));
+  for (const auto& w : withdrawals) {
+    put(fr_le(w.recipient));
+    put(Fr::from_u64(w.amount));
+  }
+  put(Fr::from_u64(withdrawals.size()));
+  for (const auto& tx : transactions) {
+    put(fr_le(tx.sender_pk));
+    put(fr_le(tx.recipient_pk));
+    put(Fr::from_u64(tx.amount));
+  }
+  put(Fr::from_u64(transactions.size()));
+  std::set<Bytes32> initial;
+  for (const auto& kv : initial_accounts) initial.insert(kv.first);
+  fold(initial);
+  return out;
 }
 
 bool R1CSMatrices::is_satisfied() const {

@@ -36,6 +36,25 @@ struct R1CSMatrices {
   bool is_satisfied() const;
 };
 
+// The witness program of one L2BlockCircuit shape (zkmi.h "witness
+// programs"): the arrays zkmi_wprog_desc points at.  Recorded once per shape
+// by synthesize(); per batch only witness_inputs() changes.  Ops used: MUL,
+// BITS (254-bit non-unique decomposition), NEQ (is_neq_const's two
+// witnesses) and POSEIDON (one permutation's S-box trace); coefficients 0..200
+// are the Poseidon constants the POSEIDON op reads.
+struct L2WitnessProgram {
+  uint64_t num_vars = 0, num_instance = 0;
+  std::vector<uint32_t> input_var;       // z index of every free input, allocation order (input 0 = One)
+  std::vector<uint32_t> op;              // 4 x u32 per op, level order
+  std::vector<uint32_t> term;            // 2 x u32 per term
+  std::vector<uint64_t> coeff;           // 4 x u64 canonical per coefficient
+  std::vector<uint32_t> level_start;     // num_levels + 1
+  std::vector<uint64_t> template_inputs; // the recorded batch's inputs (4 x u64 each)
+  size_t num_levels() const { return level_start.empty() ? 0 : level_start.size() - 1; }
+  // host evaluation of the program (test reference): canonical z, 4 x u64 per variable
+  std::vector<uint64_t> interpret(const std::vector<uint64_t>& inputs) const;
+};
+
 struct L2BlockCircuit {  // l2_circuit.rs:94-124
   Bytes32 pre_state_root{}, post_state_root{}, pre_shielded_root{}, post_shielded_root{}, withdrawal_root{},
       batch_hash{};
@@ -49,7 +68,17 @@ struct L2BlockCircuit {  // l2_circuit.rs:94-124
   // ConstraintSynthesizer::generate_constraints; `computed` receives the
   // values the circuit derives for the roots it enforces (post_state_root,
   // post_shielded_root, withdrawal_root, batch_hash, pre_state_root)
-  R1CSMatrices synthesize(std::map<std::string, Fr>* computed = nullptr) const;
+  // `prog` (optional) receives the witness program of this circuit's shape.
+  R1CSMatrices synthesize(std::map<std::string, Fr>* computed = nullptr, L2WitnessProgram* prog = nullptr) const;
+  // The R1CS structure depends only on this key: counts, and which account
+  // slots (ranks in the sorted key set, initial or created) each transfer
+  // reads and writes.  Throws synthesize's AssignmentMissing error for a
+  // sender outside the accounts.
+  std::string shape_key() const;
+  // The free inputs of this batch in the program's input order (canonical 4 x
+  // u64 each): what zkmi_wprog_run takes for a program recorded on any
+  // circuit with the same shape_key().
+  std::vector<uint64_t> witness_inputs() const;
 };
 
 // native PoseidonSponge (get_poseidon_config, l2_circuit.rs:68-83): absorb xs, squeeze one

@@ -33,6 +33,13 @@ def lib():
         L.zp_groth16_prove.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz, vp, ctypes.POINTER(ctypes.c_uint64)]
         L.zp_groth16_vk_hash.argtypes = [vp, vp]
         L.zp_groth16_free.argtypes = [vp]
+        L.zp_l2_record.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+        L.zp_l2_witness_inputs.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, ctypes.POINTER(sz)]
+        L.zp_l2_shape_key.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.c_char_p, sz]
+        L.zp_wprog_sizes.argtypes = [vp, vp]
+        L.zp_wprog_copy.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.zp_wprog_interpret.argtypes = [vp, vp, vp]
+        L.zp_wprog_free.argtypes = [vp]
         _L = L
     return _L
 
@@ -72,6 +79,117 @@ def stdrng_g1_stream(seed: int):
     rng = StdRng.seed_from_u64(seed)
     p0, d = g1_rand(rng), g1_rand(rng)
     return (np.array(_limbs(p0[0]) + _limbs(p0[1]), np.uint64), np.array(_limbs(d[0]) + _limbs(d[1]), np.uint64))
+
+
+def _encoded(inputs, witness):
+    inp, (trb, nt), (wdb, nw), (acb, na) = encode(inputs, witness)
+    keep = [_buf(inp), _buf(trb), _buf(wdb), _buf(acb)]
+    return keep, (keep[0][1], keep[1][1], nt, keep[2][1], nw, keep[3][1], na)
+
+
+def _r1cs_of_handle(L, h):
+    from .r1cs import R1CS
+    sizes = np.zeros(7, np.uint64)
+    L.zp_r1cs_sizes(h, sizes.ctypes.data)
+    m, ni, nwit = (int(x) for x in sizes[:3])
+    cs = R1CS(ni, nwit)
+    cs._m = m
+    for t, name in enumerate("abc"):
+        nnz = int(sizes[3 + t])
+        rp = np.zeros(m + 1, np.uint64)
+        col = np.zeros(max(nnz, 1), np.uint64)
+        val = np.zeros((max(nnz, 1), 4), np.uint64)
+        L.zp_r1cs_copy(h, t, rp.ctypes.data, col.ctypes.data, val.ctypes.data)
+        cs.set_csr(name, rp, col, val)
+    z = np.zeros((ni + nwit, 4), np.uint64)
+    L.zp_r1cs_z(h, z.ctypes.data)
+    return cs, z
+
+
+class L2Program:
+    """The witness program of one L2BlockCircuit shape, recorded by the C++
+    synthesizer (zp L2BlockCircuit::synthesize with an L2WitnessProgram):
+    the arrays zkmi_wprog_desc takes (zelana_amd.wprog.WitnessProgram accepts
+    this object as its plan), the recorded batch's inputs, and the host
+    interpreter (zp L2WitnessProgram::interpret) the tests compare with."""
+
+    def __init__(self, h):
+        L = lib()
+        self._h = h
+        n = np.zeros(6, np.uint64)
+        L.zp_wprog_sizes(h, n.ctypes.data)
+        self.num_vars, ni, no, nt, nc, nl = (int(x) for x in n)
+        self.num_levels = nl
+        self.input_var = np.zeros(ni, np.uint32)
+        self.op = np.zeros((max(no, 1), 4), np.uint32)[:no]
+        self.term = np.zeros((max(nt, 1), 2), np.uint32)
+        self.coeff = np.zeros((nc, 4), np.uint64)
+        self.level_start = np.zeros(nl + 1, np.uint32)
+        self.template_inputs = np.zeros((ni, 4), np.uint64)
+        L.zp_wprog_copy(h, self.input_var.ctypes.data, self.op.ctypes.data, self.term.ctypes.data,
+                        self.coeff.ctypes.data, self.level_start.ctypes.data, self.template_inputs.ctypes.data)
+        self.term = self.term[:nt]
+        self.kinds = self.op[:, 0] & 0xFF
+
+    def interpret(self, inputs: np.ndarray) -> np.ndarray:
+        inp = np.ascontiguousarray(inputs, np.uint64)
+        assert inp.shape == (self.input_var.size, 4), inp.shape
+        z = np.zeros((self.num_vars, 4), np.uint64)
+        if lib().zp_wprog_interpret(self._h, inp.ctypes.data, z.ctypes.data):
+            raise RuntimeError(lib().zp_last_error().decode())
+        return z
+
+    def stats(self) -> dict:
+        kinds = {1: "mul", 5: "bits", 6: "neq", 7: "poseidon"}
+        out = {"vars": self.num_vars, "inputs": int(self.input_var.size), "ops": int(self.op.shape[0]),
+               "levels": self.num_levels, "terms": int(self.term.shape[0]), "coefficients": int(self.coeff.shape[0])}
+        for k, name in kinds.items():
+            out[name] = int((self.kinds == k).sum())
+        return out
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().zp_wprog_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+def l2_record(inputs, witness):
+    """(R1CS, z, L2Program) of L2BlockCircuit for (inputs, witness)."""
+    L = lib()
+    keep, args = _encoded(inputs, witness)
+    h, p = vp(), vp()
+    if L.zp_l2_record(*args, ctypes.byref(h), ctypes.byref(p)):
+        raise RuntimeError(L.zp_last_error().decode())
+    try:
+        cs, z = _r1cs_of_handle(L, h)
+    finally:
+        L.zp_r1cs_free(h)
+    return cs, z, L2Program(p)
+
+
+def l2_witness_inputs(inputs, witness) -> np.ndarray:
+    """The batch's free inputs in the program's order ((n, 4) canonical u64)."""
+    L = lib()
+    keep, args = _encoded(inputs, witness)
+    n = sz()
+    if L.zp_l2_witness_inputs(*args, None, ctypes.byref(n)):
+        raise RuntimeError(L.zp_last_error().decode())
+    out = np.zeros((n.value, 4), np.uint64)
+    if L.zp_l2_witness_inputs(*args, out.ctypes.data, ctypes.byref(n)):
+        raise RuntimeError(L.zp_last_error().decode())
+    return out
+
+
+def l2_shape_key(inputs, witness) -> str:
+    L = lib()
+    keep, args = _encoded(inputs, witness)
+    buf = ctypes.create_string_buffer(1 << 16)
+    if L.zp_l2_shape_key(*args, buf, len(buf)):
+        raise RuntimeError(L.zp_last_error().decode())
+    return buf.value.decode()
 
 
 def native_l2_block_circuit(inputs, witness):
