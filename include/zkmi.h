@@ -304,8 +304,8 @@ int zkmi_proof_serialize_compressed(const uint64_t a[8], const uint64_t b[16], c
  *         <a,z>: z[out + 4r + (0..3)] = t_r^2, t_r^4, t_r^6, t_r^7 (91 rounds,
  *         t_0 = <a,z> + c_0, t_r = t_{r-1}^7 + c_r, c_i = (i+1)^3 + (i+1))
  *         5 BITS z[out+i] = bit i of <a,z>, i < b_off (1..256; b_len = 0);
- *         6 NEQ z[out] = (<a,z> != 0), z[out+1] = <a,z>^-1, or 1 when it is 0
- *         (r1cs-std is_neq's two witnesses);
+ *         6 NZ z[out] = (<a,z> != 0); 8 INV1 z[out] = <a,z>^-1, or 1 when it
+ *         is 0 (r1cs-std is_neq's two witnesses);
  *         7 POSEIDON one permutation of L2BlockCircuit's width-3 Poseidon
  *         sponge (prover/src/l2_circuit.rs:68-83: x^5, 8 full + 56 partial
  *         rounds).  State in: three combinations stored back to back at

@@ -3,7 +3,7 @@
 The C++ synthesizer (zelana_amd/host/l2_circuit.cpp, restating
 prover/src/l2_circuit.rs:180-505) records, once per circuit shape, the
 straight-line program that computes the full assignment z from a batch's free
-inputs: MUL / BITS / NEQ ops and one POSEIDON op per sponge permutation
+inputs: MUL / BITS / NZ / INV1 ops and one POSEIDON op per sponge permutation
 (l2_circuit.rs:68-83).  Per batch only the inputs are extracted
 (L2BlockCircuit::witness_inputs) and the GPU runs the program (wprog.hip).
 
@@ -71,10 +71,14 @@ def test_program_levels_and_layout():
     _, _, prog = H.l2_record(inp, w)
     ls = prog.level_start
     assert ls[0] == 0 and ls[-1] == prog.op.shape[0] and (np.diff(ls.astype(np.int64)) > 0).all()
-    # every level is all permutations or none (one launch kind per level)
+    # permutations lead their level (the launch kind is read from its first op)
     for lo, hi in zip(ls[:-1], ls[1:]):
         k = prog.kinds[lo:hi]
-        assert (k == 7).all() or not (k == 7).any()
+        npos = int((k == 7).sum())
+        assert (k[:npos] == 7).all()
+    # the is_neq multipliers (unread inversions) all wait for the last launch
+    inv = np.nonzero(prog.kinds == 8)[0]
+    assert inv.size and (inv >= ls[-2]).all()
     # the Poseidon constants lead the coefficient table (zkmi.h POSEIDON)
     assert prog.coeff.shape[0] >= 201
     assert (prog.input_var[0] == 0) and (prog.template_inputs[0] == [1, 0, 0, 0]).all()

@@ -17,7 +17,8 @@
 // and, for L2BlockCircuit (prover/src/l2_circuit.rs:180-505, recorded by the
 // C++ synthesizer, zelana_amd/host/l2_circuit.cpp):
 //   BITS   z[out + i] = bit i of <a, z>, i < n     (to_non_unique_bits_le)
-//   NEQ    z[out] = (<a, z> != 0), z[out + 1] = <a, z>^-1 or 1   (is_neq)
+//   NZ     z[out] = (<a, z> != 0)                  (is_neq's flag)
+//   INV1   z[out] = <a, z>^-1, or 1 for 0         (is_neq's multiplier)
 //   POSEIDON  one permutation of the width-3 sponge (l2_circuit.rs:68-83:
 //          x^5, 8 full + 56 partial rounds, Grain-LFSR constants): state in =
 //          three combinations, out = every S-box's x^2, x^4, x^5 in round
@@ -49,7 +50,8 @@
 
 namespace zk {
 
-constexpr int WP_MUL = 1, WP_INV = 2, WP_BITS64 = 3, WP_PERM = 4, WP_BITS = 5, WP_NEQ = 6, WP_POSEIDON = 7;
+constexpr int WP_MUL = 1, WP_INV = 2, WP_BITS64 = 3, WP_PERM = 4, WP_BITS = 5, WP_NZ = 6, WP_POSEIDON = 7,
+              WP_INV1 = 8;
 constexpr int MIMC_R = 91;
 // Poseidon (get_poseidon_config): constants at coefficient ids 3 r + i (ark)
 // and 192 + 3 i + j (MDS) of the program's table (zkmi.h)
@@ -276,10 +278,12 @@ __device__ __forceinline__ void poseidon_quad(const Fe& in, uint32_t q, uint32_t
       } else {
         at = m0 + 27 + 3 * (POS_ROUNDS - 2 * POS_FULL_HALF) + 9 * (r - (POS_ROUNDS - POS_FULL_HALF)) + 3 * q;
       }
-      if (st) {
-        st_canon(z, out + at, redc_fr(x2));
-        st_canon(z, out + at + 1, redc_fr(x4));
-        st_canon(z, out + at + 2, redc_fr(x5));
+      if (st) {  // Montgomery form (k_wprog_canon_vars converts them at the end of the run), except
+                 // the last round's x^5, which the next permutations' state combinations read
+        st_raw(z, out + at, x2);
+        st_raw(z, out + at + 1, x4);
+        if (r == POS_ROUNDS - 1) st_canon(z, out + at + 2, redc_fr(x5));
+        else st_raw(z, out + at + 2, x5);
       }
     }
     const Fe b0 = quad_bcast<0>(u), b1 = quad_bcast<1>(u), b2 = quad_bcast<2>(u);
@@ -288,28 +292,11 @@ __device__ __forceinline__ void poseidon_quad(const Fe& in, uint32_t q, uint32_t
   }
 }
 
+// One op of a level, on the quad of lanes (op_i, q).
 template <bool POS>
-__global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ ops, uint32_t lo, uint32_t hi,
-                                                     const uint2* __restrict__ terms,
-                                                     const uint32_t* __restrict__ coeff_m,
-                                                     const uint32_t* __restrict__ rc_m, uint32_t* __restrict__ z,
-                                                     size_t zstride) {
-  z += blockIdx.y * zstride;  // batch blockIdx.y of a multi-batch run
-  // Round constants in LDS: a global load inside the round loop would make
-  // every round wait (vmcnt) for the previous round's stores to land.
-  __shared__ uint32_t rc_s[MIMC_R * 8];
-  __shared__ Fe pc_s[POS ? POS_NCONST : 1];  // Poseidon constants, unpacked Montgomery
-  for (uint32_t i = threadIdx.x; i < MIMC_R * 8; i += blockDim.x) rc_s[i] = rc_m[i];
-  if constexpr (POS)
-    for (uint32_t i = threadIdx.x; i < POS_NCONST; i += blockDim.x) pc_s[i] = ld_canon(coeff_m, i);
-  __syncthreads();
-  // The program runs beside a proof whose MSM waves fill the same SIMDs:
-  // top wave priority wins the VALU arbitration for this latency-critical
-  // chain (a handful of waves against the proof's thousands)
-  __builtin_amdgcn_s_setprio(3);
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t op_i = lo + (t >> 2), q = t & 3;
-  if (op_i >= hi) return;
+__device__ __forceinline__ void wprog_op(uint32_t op_i, uint32_t q, const uint4* __restrict__ ops,
+                                         const uint2* __restrict__ terms, const uint32_t* __restrict__ coeff_m,
+                                         const uint32_t* rc_s, const Fe* pc_s, uint32_t* __restrict__ z) {
   const uint4 op = ops[op_i];
   const int kind = op.x & 0xFF;
   const uint32_t alen = (op.x >> 8) & 0xFFF, blen = op.x >> 20, out = op.y;
@@ -358,28 +345,75 @@ __global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ o
   if (kind == WP_MUL) {
     const Fe b = eval_lc(terms, op.w, blen, coeff_m, z);
     st_canon(z, out, mul<FrP>(mul<FrP>(a, fe_const<FrP>(FrP::R2)), b));
-  } else if (kind == WP_INV || kind == WP_NEQ) {
-    // r - 2 (Fermat); 0 stays 0
+  } else if (kind == WP_NZ) {
+    const Fe ar = reduce<FrP>(a);
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < NL; i++) nz |= ar.v[i];
+    Fe ne = fe_zero();
+    ne.v[0] = nz != 0;
+    st_canon(z, out, ne);
+  } else if (kind == WP_INV || kind == WP_INV1) {
+    // r - 2 (Fermat); 0 stays 0 (INV) or becomes 1 (INV1)
     const uint64_t e[4] = {0x43e1f593efffffffULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL,
                            0x30644e72e131a029ULL};
     const Fe am = mul<FrP>(a, fe_const<FrP>(FrP::R2));
     Fe inv = redc_fr(reduce<FrP>(pow<FrP>(am, e)));
-    if (kind == WP_NEQ) {
-      // is_neq_const's witnesses: ne, then ne ? 1 / a : 1
-      const Fe ar = reduce<FrP>(a);
+    if (kind == WP_INV1) {
       uint32_t nz = 0;
 #pragma unroll
-      for (int i = 0; i < NL; i++) nz |= ar.v[i];
-      Fe one_v = fe_zero();
-      one_v.v[0] = 1;
-      Fe ne = fe_zero();
-      ne.v[0] = nz != 0;
-      st_canon(z, out, ne);
-      if (!nz) inv = one_v;
-      st_canon(z, out + 1, inv);
-    } else {
-      st_canon(z, out, inv);
+      for (int i = 0; i < NL; i++) nz |= inv.v[i];
+      if (!nz) inv.v[0] = 1;
     }
+    st_canon(z, out, inv);
+  }
+}
+
+template <bool POS>
+__global__ void __launch_bounds__(256) k_wprog_level(const uint4* __restrict__ ops, uint32_t lo, uint32_t hi,
+                                                     const uint2* __restrict__ terms,
+                                                     const uint32_t* __restrict__ coeff_m,
+                                                     const uint32_t* __restrict__ rc_m, uint32_t* __restrict__ z,
+                                                     size_t zstride) {
+  z += blockIdx.y * zstride;  // batch blockIdx.y of a multi-batch run
+  // Round constants in LDS: a global load inside the round loop would make
+  // every round wait (vmcnt) for the previous round's stores to land.
+  __shared__ uint32_t rc_s[MIMC_R * 8];
+  __shared__ Fe pc_s[POS ? POS_NCONST : 1];  // Poseidon constants, unpacked Montgomery
+  for (uint32_t i = threadIdx.x; i < MIMC_R * 8; i += blockDim.x) rc_s[i] = rc_m[i];
+  if constexpr (POS)
+    for (uint32_t i = threadIdx.x; i < POS_NCONST; i += blockDim.x) pc_s[i] = ld_canon(coeff_m, i);
+  __syncthreads();
+  // The program runs beside a proof whose MSM waves fill the same SIMDs:
+  // top wave priority wins the VALU arbitration for this latency-critical
+  // chain (a handful of waves against the proof's thousands)
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t op_i = lo + (t >> 2), q = t & 3;
+  if (op_i >= hi) return;
+  wprog_op<POS>(op_i, q, ops, terms, coeff_m, rc_s, pc_s, z);
+}
+
+// A run of consecutive small levels without permutations (the comparison
+// gadgets' MUL / NZ chains: dozens of levels of a few ops each) in ONE
+// launch: one 1024-thread workgroup per batch steps through the levels with a
+// barrier between them (global stores of a level are visible to the whole
+// workgroup after it), instead of one launch per level.
+__global__ void __launch_bounds__(1024) k_wprog_chain(const uint4* __restrict__ ops,
+                                                      const uint32_t* __restrict__ level_start, uint32_t l0,
+                                                      uint32_t l1, const uint2* __restrict__ terms,
+                                                      const uint32_t* __restrict__ coeff_m,
+                                                      const uint32_t* __restrict__ rc_m, uint32_t* __restrict__ z,
+                                                      size_t zstride) {
+  z += blockIdx.y * zstride;
+  __shared__ uint32_t rc_s[MIMC_R * 8];
+  for (uint32_t i = threadIdx.x; i < MIMC_R * 8; i += blockDim.x) rc_s[i] = rc_m[i];
+  __builtin_amdgcn_s_setprio(3);
+  for (uint32_t l = l0; l < l1; l++) {
+    __syncthreads();
+    const uint32_t lo = level_start[l], hi = level_start[l + 1];
+    for (uint32_t op_i = lo + (threadIdx.x >> 2); op_i < hi; op_i += blockDim.x >> 2)
+      wprog_op<false>(op_i, threadIdx.x & 3, ops, terms, coeff_m, rc_s, nullptr, z);
   }
 }
 
@@ -393,6 +427,15 @@ __global__ void __launch_bounds__(256) k_wprog_canon(const uint32_t* __restrict_
   if (i >= nperm * PER) return;
   const uint32_t var = perm_out[i / PER] + i % PER;
   st_canon(z, var, redc_fr(ld_canon(z, var)));
+}
+
+// Montgomery -> canonical for a list of variables (Poseidon traces)
+__global__ void __launch_bounds__(256) k_wprog_canon_vars(const uint32_t* __restrict__ vars, uint32_t n,
+                                                          uint32_t* __restrict__ z, size_t zstride) {
+  z += blockIdx.y * zstride;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  st_canon(z, vars[i], redc_fr(ld_canon(z, vars[i])));
 }
 
 __global__ void __launch_bounds__(256) k_wprog_inputs(const uint32_t* __restrict__ in, const uint32_t* __restrict__ var,
@@ -426,6 +469,9 @@ struct zkmi_wprog {
   uint4* d_ops = nullptr;
   uint2* d_terms = nullptr;
   uint32_t* d_perm_out = nullptr;  // first trace variable of every permutation
+  uint32_t* d_level_start = nullptr;
+  uint32_t* d_raw = nullptr;  // Poseidon trace variables stored in Montgomery form
+  uint32_t num_raw = 0;
   uint32_t num_perms = 0;
   std::vector<uint32_t> level_start;  // host: op ranges per level
   std::vector<uint32_t> op_kinds;     // host: kinds (level geometry)
@@ -449,6 +495,8 @@ static void wprog_free(zkmi_wprog* p) {
   (void)hipFree(p->d_ops);
   (void)hipFree(p->d_terms);
   (void)hipFree(p->d_perm_out);
+  (void)hipFree(p->d_level_start);
+  (void)hipFree(p->d_raw);
   for (int b = 0; b < 2; b++) {
     if (p->h_in[b]) (void)hipHostFree(p->h_in[b]);
     if (p->in_done[b]) (void)hipEventDestroy(p->in_done[b]);
@@ -495,15 +543,15 @@ int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* d, zkmi_wprog** out)
   for (size_t i = 0; i < d->num_ops; i++) {
     const uint32_t* o = d->op + 4 * i;
     const uint32_t kind = o[0] & 0xFF, alen = (o[0] >> 8) & 0xFFF, blen = o[0] >> 20;
-    bool ok = kind >= WP_MUL && kind <= WP_POSEIDON;
+    bool ok = kind >= WP_MUL && kind <= WP_INV1;
     uint64_t span = 1;
     if (kind == WP_POSEIDON) {
       const uint32_t l2 = o[3] & 0xFFFF, mask = o[3] >> 16;
       span = poseidon_trace_len(mask);
-      ok = ok && mask >= 1 && mask <= 7 && l2 < 4096 && (uint64_t)o[2] + alen + blen + l2 <= d->num_terms &&
+      ok = ok && kind != 0 && mask >= 1 && mask <= 7 && l2 < 4096 && (uint64_t)o[2] + alen + blen + l2 <= d->num_terms &&
            d->num_coeffs >= (size_t)POS_NCONST;
     } else {
-      span = kind == WP_PERM ? 4 * MIMC_R : kind == WP_BITS64 ? 64 : kind == WP_BITS ? o[3] : kind == WP_NEQ ? 2 : 1;
+      span = kind == WP_PERM ? 4 * MIMC_R : kind == WP_BITS64 ? 64 : kind == WP_BITS ? o[3] : 1;
       ok = ok && (uint64_t)o[2] + alen <= d->num_terms && (kind == WP_MUL ? (uint64_t)o[3] + blen <= d->num_terms : !blen) &&
            (kind != WP_BITS || (o[3] >= 1 && o[3] <= 256));
     }
@@ -554,12 +602,42 @@ int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* d, zkmi_wprog** out)
   std::vector<uint32_t> perm_out;
   for (size_t i = 0; i < d->num_ops; i++)
     if (kinds[i] == WP_PERM) perm_out.push_back(d->op[4 * i + 1]);
+  // Poseidon traces are stored in Montgomery form but for the last round's
+  // x^5 values; no op may read the others
+  std::vector<uint32_t> raw;
+  {
+    std::vector<uint8_t> is_raw(d->num_vars, 0);
+    for (size_t i = 0; i < d->num_ops; i++) {
+      if (kinds[i] != WP_POSEIDON) continue;
+      const uint32_t out = d->op[4 * i + 1], len = poseidon_trace_len(d->op[4 * i + 3] >> 16);
+      for (uint32_t k = 0; k < len; k++) {
+        const bool final_x5 = k >= len - 9 && (k - (len - 9)) % 3 == 2;
+        if (!final_x5) {
+          is_raw[out + k] = 1;
+          raw.push_back(out + k);
+        }
+      }
+    }
+    for (size_t i = 0; i < d->num_terms && !raw.empty(); i++)
+      if (is_raw[d->term[2 * i]]) {
+        set_error("zkmi_wprog_create: term %zu reads a Poseidon trace value other than the output round's x^5", i);
+        wprog_free(p);
+        return ZKMI_EINVAL;
+      }
+  }
   p->num_perms = (uint32_t)perm_out.size();
   const size_t ni = d->num_inputs, no = std::max<size_t>(1, d->num_ops), nt = std::max<size_t>(1, d->num_terms);
   if (hipMalloc(&p->d_perm_out, std::max<size_t>(1, perm_out.size()) * 4) != hipSuccess ||
       (!perm_out.empty() && hipMemcpy(p->d_perm_out, perm_out.data(), perm_out.size() * 4, hipMemcpyHostToDevice) !=
                                 hipSuccess))
     return fail("permutation list");
+  p->num_raw = (uint32_t)raw.size();
+  if (hipMalloc(&p->d_raw, std::max<size_t>(1, raw.size()) * 4) != hipSuccess ||
+      (!raw.empty() && hipMemcpy(p->d_raw, raw.data(), raw.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+    return fail("Poseidon trace list");
+  if (hipMalloc(&p->d_level_start, (d->num_levels + 1) * 4) != hipSuccess ||
+      hipMemcpy(p->d_level_start, d->level_start, (d->num_levels + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return fail("level list");
   if (hipMalloc(&p->d_input_var, ni * 4) != hipSuccess || hipMalloc(&p->d_in, ni * 32) != hipSuccess ||
       hipMalloc(&p->d_ops, no * 16) != hipSuccess || hipMalloc(&p->d_terms, nt * 8) != hipSuccess ||
       hipMalloc(&p->d_coeff, d->num_coeffs * 32) != hipSuccess || hipMalloc(&p->d_rc, MIMC_R * 32) != hipSuccess ||
@@ -636,19 +714,39 @@ int zkmi_wprog_run_many(zkmi_ctx* ctx, zkmi_wprog* p, size_t nb, const uint64_t*
   ZK_HIP(hipEventRecord(p->in_done[b], st));
   k_wprog_inputs<<<dim3((unsigned)((p->num_inputs + 255) / 256), nby), 256, 0, st>>>(
       p->d_in, p->d_input_var, (uint32_t)p->num_inputs, z, zs);
-  for (size_t l = 0; l + 1 < p->level_start.size(); l++) {
+  const size_t nl = p->level_start.size() - 1;
+  // chainable: no permutation (they sort first in their level), one pass of
+  // a 1024-thread workgroup
+  auto chainable = [&](size_t l) {
     const uint32_t lo = p->level_start[l], hi = p->level_start[l + 1];
-    if (hi == lo) continue;
+    return hi > lo && hi - lo <= 256 && p->op_kinds[lo] != WP_PERM && p->op_kinds[lo] != WP_POSEIDON;
+  };
+  for (size_t l = 0; l < nl;) {
+    const uint32_t lo = p->level_start[l], hi = p->level_start[l + 1];
+    if (hi == lo) {
+      l++;
+      continue;
+    }
+    size_t l1 = l;
+    while (l1 < nl && chainable(l1)) l1++;
+    if (l1 - l >= 2) {
+      k_wprog_chain<<<dim3(1, nby), 1024, 0, st>>>(p->d_ops, p->d_level_start, (uint32_t)l, (uint32_t)l1, p->d_terms,
+                                                   p->d_coeff, p->d_rc, z, zs);
+      l = l1;
+      continue;
+    }
     const size_t threads = (size_t)(hi - lo) * 4;
-    // permutations sort first in their level
     auto kern = p->op_kinds[lo] == WP_POSEIDON ? k_wprog_level<true> : k_wprog_level<false>;
     kern<<<dim3((unsigned)((threads + 255) / 256), nby), 256, 0, st>>>(p->d_ops, lo, hi, p->d_terms, p->d_coeff,
                                                                        p->d_rc, z, zs);
+    l++;
   }
   if (p->num_perms) {
     const size_t nconv = (size_t)p->num_perms * (4 * MIMC_R - 1);
     k_wprog_canon<<<dim3((unsigned)((nconv + 255) / 256), nby), 256, 0, st>>>(p->d_perm_out, p->num_perms, z, zs);
   }
+  if (p->num_raw)
+    k_wprog_canon_vars<<<dim3((p->num_raw + 255) / 256, nby), 256, 0, st>>>(p->d_raw, p->num_raw, z, zs);
   ZK_HIP(hipGetLastError());
   ZK_HIP(hipEventRecord(p->done, st));
   // later context work (the proofs over these z) waits for the witness

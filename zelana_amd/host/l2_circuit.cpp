@@ -133,7 +133,7 @@ LC lc_scale(const LC& a, const Fr& c) {
 }
 
 // witness-program op kinds (zkmi.h)
-constexpr uint32_t WP_MUL = 1, WP_BITS = 5, WP_NEQ = 6, WP_POSEIDON = 7;
+constexpr uint32_t WP_MUL = 1, WP_INV = 2, WP_BITS = 5, WP_NZ = 6, WP_POSEIDON = 7, WP_INV1 = 8;
 
 struct CS {
   std::vector<Fr> inst{Fr::one()}, wit;
@@ -275,7 +275,8 @@ Boolean is_neq_const(const FpVar& x, const Fr& c) {
   Boolean nb{cs, false, cs->new_witness(Fr::from_u64(ne)), ne};
   FpVar mult = FpVar::witness(cs, ne ? d.inverse() : Fr::one());
   const LC diff = lc_add(one_lc(c), x.term(), true);
-  cs->op(WP_NEQ, nb.lc[0].first, {diff});  // nb, then mult
+  cs->op(WP_NZ, nb.lc[0].first, {diff});
+  cs->op(WP_INV1, mult.lc[0].first, {diff});
   cs->enforce(diff, mult.lc, nb.lc);
   cs->enforce(diff, nb.negate().term(), LC{});
   return nb;
@@ -612,8 +613,8 @@ uint64_t op_span(uint32_t kind, uint32_t aux) {
   switch (kind) {
     case WP_MUL: return 1;
     case WP_BITS: return aux;
-    case WP_NEQ: return 2;
-    default: return 3 * (uint64_t)__builtin_popcount(aux) + 231;  // POSEIDON
+    case WP_POSEIDON: return 3 * (uint64_t)__builtin_popcount(aux) + 231;
+    default: return 1;
   }
 }
 
@@ -697,6 +698,22 @@ void build_program(const CS& cs, L2WitnessProgram& P) {
   }
   for (uint64_t v = 0; v < nv; v++)
     if (!produced[v]) throw std::logic_error("witness program: variable neither input nor op output");
+  // Inversions nothing reads (is_neq's multipliers, constraint-only) run in
+  // the last launch, beside the permutations, instead of lengthening the
+  // comparison chains they hang off (each is a ~250-squaring exponentiation).
+  std::vector<uint8_t> read(nv, 0);
+  uint64_t last = 0;
+  for (size_t i = 0; i < cs.ops.size(); i++) {
+    for (const LC& lc : cs.ops[i].lcs)
+      for (const auto& t : lc)
+        if (!t.second.is_zero()) read[zidx(t.first)] = 1;
+    last = std::max(last, order[i].key);
+  }
+  for (size_t i = 0; i < cs.ops.size(); i++)
+    if ((cs.ops[i].kind == WP_INV1 || cs.ops[i].kind == WP_INV) && !read[zidx(cs.ops[i].out)]) {
+      order[i].key = last;
+      order[i].pos = false;
+    }
   // within a level: permutations first (the quads of one wave share a kind)
   std::stable_sort(order.begin(), order.end(), [](const Sched& a, const Sched& b) {
     return a.key != b.key ? a.key < b.key : (a.pos && !b.pos);
@@ -755,10 +772,11 @@ std::vector<uint64_t> L2WitnessProgram::interpret(const std::vector<uint64_t>& i
     } else if (kind == WP_BITS) {
       const Fr a = ev(o[2], la);
       for (uint32_t b = 0; b < o[3]; b++) z[out + b] = Fr::from_u64(a.bit((int)b));
-    } else if (kind == WP_NEQ) {
+    } else if (kind == WP_NZ) {
+      z[out] = Fr::from_u64(!ev(o[2], la).is_zero());
+    } else if (kind == WP_INV1 || kind == WP_INV) {
       const Fr a = ev(o[2], la);
-      z[out] = Fr::from_u64(!a.is_zero());
-      z[out + 1] = a.is_zero() ? Fr::one() : a.inverse();
+      z[out] = a.is_zero() ? (kind == WP_INV1 ? Fr::one() : Fr()) : a.inverse();
     } else if (kind == WP_POSEIDON) {
       const uint32_t l2 = o[3] & 0xFFFF, mask = o[3] >> 16;
       Fr st[3] = {ev(o[2], la), ev(o[2] + la, lb), ev(o[2] + la + lb, l2)};

@@ -39,7 +39,7 @@ struct R1CSMatrices {
 // The witness program of one L2BlockCircuit shape (zkmi.h "witness
 // programs"): the arrays zkmi_wprog_desc points at.  Recorded once per shape
 // by synthesize(); per batch only witness_inputs() changes.  Ops used: MUL,
-// BITS (254-bit non-unique decomposition), NEQ (is_neq_const's two
+// BITS (254-bit non-unique decomposition), NZ and INV1 (is_neq_const's two
 // witnesses) and POSEIDON (one permutation's S-box trace); coefficients 0..200
 // are the Poseidon constants the POSEIDON op reads.
 struct L2WitnessProgram {

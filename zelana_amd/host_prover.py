@@ -140,7 +140,7 @@ class L2Program:
         return z
 
     def stats(self) -> dict:
-        kinds = {1: "mul", 5: "bits", 6: "neq", 7: "poseidon"}
+        kinds = {1: "mul", 5: "bits", 6: "nz", 7: "poseidon", 8: "inv1"}
         out = {"vars": self.num_vars, "inputs": int(self.input_var.size), "ops": int(self.op.shape[0]),
                "levels": self.num_levels, "terms": int(self.term.shape[0]), "coefficients": int(self.coeff.shape[0])}
         for k, name in kinds.items():
