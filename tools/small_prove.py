@@ -26,6 +26,10 @@ def main():
     from zelana_amd.rng import StdRng
 
     ctx = gpu.Context(0)
+    if os.environ.get("SP_LANES"):
+        ctx.set_lanes(int(os.environ["SP_LANES"]))
+    if os.environ.get("SP_WINDOW"):
+        ctx.set_window(int(os.environ["SP_WINDOW"]))
     cs0, _, _ = L2BlockCircuit.dummy().synthesize()
     pk, vk = circuit_specific_setup(ctx, cs0, StdRng.seed_from_u64(0))
     pk.precompute()
@@ -49,6 +53,10 @@ def main():
         res = gpu.groth16_prove_resident(ctx, pk, dev, dz, r, s)
         t.append(time.perf_counter() - t0)
     out["resident_ms"] = [round(1e3 * float(np.median(t)), 3), round(1e3 * min(t), 3)]
+    out["resident_proof"] = np.concatenate([np.asarray(x).ravel() for x in res]).tobytes().hex()[:16]
+    if os.environ.get("SP_RESIDENT_ONLY"):
+        print(out, {k: v for k, v in os.environ.items() if k.startswith(("SP_", "ZKMI_"))}, flush=True)
+        return
     native = NativeGroth16Prover(pk.serialize(), vk, ctx.device)
     for mode in ("wprog", "host"):
         if mode == "host":
@@ -63,6 +71,7 @@ def main():
         out[f"native_{mode}_ms"] = [round(1e3 * float(np.median(t)), 3), round(1e3 * min(t), 3)]
         out[f"native_{mode}_bytes"] = first.hex()[:16]
     os.environ.pop("ZP_HOST_SYNTH", None)
+    out["env"] = {k: v for k, v in os.environ.items() if k.startswith(("SP_", "ZKMI_"))}
     print(out, flush=True)
     native.close()
 

@@ -1292,8 +1292,12 @@ int zkmi_pk_precompute(zkmi_pk* pk, int factor) {
   const bool compact = pk->d_bidx != nullptr;
   zkmi_bases* qs[5] = {pk->h_query_rev, pk->l_query, pk->a_query, compact ? pk->b_g1_c : pk->b_g1_query,
                        compact ? pk->b_g2_c : pk->b_g2_query};
+  static const size_t min_n = [] {  // experiments: queries below this many bases get no table
+    const char* e = getenv("ZKMI_PK_TABLE_MIN");
+    return e ? (size_t)atoll(e) : (size_t)0;
+  }();
   for (zkmi_bases* b : qs) {
-    if (!b || b->tc) continue;
+    if (!b || b->tc || b->n < min_n) continue;
     int rc = zk::bases_precompute(b, zk::table_window(b->n, b->g2), factor);
     if (rc) return rc;
   }
