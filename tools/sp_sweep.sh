@@ -13,3 +13,5 @@ run ZKMI_PK_TABLE_MIN=100000 SP_LANES=3 SP_WINDOW=8
 run ZKMI_PK_TABLE_MIN=100000 SP_LANES=3 SP_WINDOW=9
 run ZKMI_TABLE_C=16 SP_LANES=3
 run ZKMI_TABLE_C=10 SP_LANES=3
+run ZKMI_LIB=zelana_amd/_ab/libzkmi_noasm.so SP_LANES=2
+run ZKMI_LIB=zelana_amd/_ab/libzkmi_noasm.so SP_LANES=3

@@ -788,6 +788,55 @@ struct zkmi_proof_job {
 namespace zk {
 
 // ------------------------------------------------------------ prove
+// Small proofs (configs[0]: a 2^13 domain) are latency-bound: every kernel
+// of an MSM is a short dependent chain, and enqueueing the ~130 launches of
+// a proof costs the host about a millisecond.  So the order favours the
+// critical paths: the witness map (feeding the h MSM) is queued first on the
+// context stream, the B MSMs (the G2 one is the longest chain) next on a lane
+// of their own, then l, a and h on the other lane; all z-weighted MSMs fork
+// from one event recorded before the witness map, so they run beside it.
+static size_t small_proof_max() {
+  static const size_t v = [] {
+    const char* e = getenv("ZKMI_SMALL_PROOF_MAX");  // domain size up to which the small schedule applies
+    return e ? (size_t)atoll(e) : (size_t)1 << 16;
+  }();
+  return v;
+}
+static int prove_submit_small(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
+                              uint32_t logn, uint32_t* dh, zkmi_msm_job** jobs) {
+  const size_t l = dr.l, w = dr.w, nv = l + w, n = pk->n;
+  const int nl = std::max(1, ctx->msm_lanes);
+  if (!ctx->prove_fork) ZK_HIP(hipEventCreateWithFlags(&ctx->prove_fork, hipEventDisableTiming));
+  uint32_t* zb = nullptr;
+  if (pk->d_bidx) {
+    ZK_TRY(ctx->ws.get("g16_zb", pk->nb_c * 32, (void**)&zb));
+    k_gather_scalars<<<(unsigned)((pk->nb_c + 255) / 256), 256, 0, ctx->stream>>>(dz, pk->d_bidx, pk->nb_c, zb);
+    ZK_HIP(hipGetLastError());
+  }
+  ZK_HIP(hipEventRecord(ctx->prove_fork, ctx->stream));
+  ZK_TRY(witness_map_dev(ctx, dr, dz, logn, dh));
+  ctx->msm_fork = ctx->prove_fork;
+  int rc = 0;
+  ctx->lane_next = 0;
+  if (pk->d_bidx) {
+    const zkmi_bases* bq[2] = {pk->b_g1_c, pk->b_g2_c};
+    rc = msm_submit_shared(ctx, bq, 2, 0, zb, pk->nb_c, &jobs[3]);
+    ctx->lane_next = 1 % nl;
+    if (!rc) rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
+    ctx->lane_next = (nl >= 3 ? 2 : 1) % nl;
+    if (!rc) rc = msm_submit(ctx, pk->a_query, 1, dz + 8, nv - 1, &jobs[2]);
+  } else {
+    const zkmi_bases* abq[3] = {pk->a_query, pk->b_g1_query, pk->b_g2_query};
+    rc = msm_submit_shared(ctx, abq, 3, 1, dz + 8, nv - 1, &jobs[2]);
+    ctx->lane_next = 1 % nl;
+    if (!rc) rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
+  }
+  ctx->msm_fork = nullptr;  // h forks after the witness map
+  ctx->lane_next = 1 % nl;
+  if (!rc) rc = msm_submit(ctx, pk->h_query_rev, 0, dh, n - 1, &jobs[0]);
+  return rc;
+}
+
 // core: R1CS and full assignment z already resident in HBM.  submit queues
 // everything (the witness map on the context stream, the MSMs on the lanes)
 // and returns; several proofs may be in flight, finished in order by wait.
@@ -817,6 +866,9 @@ int groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, co
   zkmi_msm_job** jobs = pj->jobs;
   for (int i = 0; i < 5; i++) jobs[i] = nullptr;
   int rc = 0;
+  if (n <= small_proof_max()) {
+    rc = prove_submit_small(ctx, pk, dr, dz, logn, dh, jobs);
+  } else {
   rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
   if (!rc && pk->d_bidx) {  // a over z[1..V]; b1 / b2 over the compacted B variables
     uint32_t* zb;
@@ -834,6 +886,7 @@ int groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, co
   }
   if (!rc) rc = witness_map_dev(ctx, dr, dz, logn, dh);
   if (!rc) rc = msm_submit(ctx, pk->h_query_rev, 0, dh, n - 1, &jobs[0]);
+  }
   if (rc) {
     for (auto* j : pj->jobs)
       if (j) msm_job_free(j);

@@ -705,6 +705,73 @@ __global__ void __launch_bounds__(256) k_msm_cutsum(const uint32_t* __restrict__
   st_xyzz<G>(buckets + (size_t)b * XW, sum);
 }
 
+// Small MSMs (K <= 2^16 buckets: the proofs of configs[0]) are latency-
+// bound: k_msm_cutsum's one thread per bucket adds up to ACC_KMAX - 1 pieces
+// in a dependent chain (~10 curve additions, ~130 us for G1 and ~400 us for
+// G2 at a 2^13 domain).  Here 16 lanes share a bucket and add its <= 16
+// pieces as a butterfly tree over lane shuffles: 4 dependent additions.
+// Same group element per bucket (the XYZZ representative may differ; every
+// consumer is representation-independent).
+__device__ __forceinline__ Fe shfl_xor_fe(const Fe& a, int m) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], m, 16);
+  return r;
+}
+__device__ __forceinline__ Fe2 shfl_xor_fe(const Fe2& a, int m) { return {shfl_xor_fe(a.c0, m), shfl_xor_fe(a.c1, m)}; }
+template <class F>
+__device__ __forceinline__ Xyzz<F> shfl_xor_xyzz(const Xyzz<F>& a, int m) {
+  Xyzz<F> r;
+  r.x = shfl_xor_fe(a.x, m);
+  r.y = shfl_xor_fe(a.y, m);
+  r.zz = shfl_xor_fe(a.zz, m);
+  r.zzz = shfl_xor_fe(a.zzz, m);
+  return r;
+}
+constexpr uint32_t CUTSUM_COOP_K = 1u << 16;  // bucket counts up to which the tree form runs
+template <class G>
+__global__ void __launch_bounds__(256) k_msm_cutsum_coop(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t L,
+                                                         uint32_t* __restrict__ buckets,
+                                                         uint32_t* __restrict__ xvalid,
+                                                         const uint32_t* __restrict__ xpts,
+                                                         uint32_t* __restrict__ open_flag) {
+  using F = typename G::F;
+  constexpr int XW = 4 * G::CW;
+  const uint32_t gt = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t b = gt >> 4, r = gt & 15;
+  // every lane stays to the end: the shuffles need the whole group
+  bool live = b < K;
+  uint32_t t0 = 0, k = 0;
+  if (live) {
+    const uint32_t lo = bstart[b], hi = bstart[b + 1];
+    live = hi - lo >= 2;
+    if (live) {
+      t0 = lo / L;
+      k = (hi - 1) / L - t0 + 1;
+      live = k > 1;  // else complete inside one chunk: already in buckets[b]
+    }
+  }
+  if (live && k > 16) {  // left to the k_msm_accN cascade
+    if (r == 0) atomicOr(open_flag, 1u);
+    live = false;
+  }
+  bool has = live && r < k;
+  Xyzz<F> v = xyzz_inf<F>();
+  if (has) {
+    const uint32_t slot = r == 0 ? 2 * t0 + 2 : 2 * (t0 + r) + 1;  // tail of chunk t0, heads of t0+1..
+    v = ld_xyzz<G>(xpts + (size_t)slot * XW);
+    xvalid[slot] = 0;
+  }
+#pragma unroll 1
+  for (int m = 1; m < 16; m <<= 1) {
+    const Xyzz<F> o = shfl_xor_xyzz(v, m);
+    const bool oh = __shfl_xor((int)has, m, 16) != 0;
+    if ((r & m) == 0 && oh) v = has ? br_add<G>(v, o) : o;
+    has = has || oh;
+  }
+  if (live && r == 0) st_xyzz<G>(buckets + (size_t)b * XW, v);
+}
+
 // accumulator store: G1 keeps X lazily in [0, 8p) inside the loop
 template <class G>
 __device__ __forceinline__ void st_acc(uint32_t* p, Xyzz<typename G::F> v) {
@@ -2462,8 +2529,12 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   ZK_TRY(ws.get("msm_tstart", (size_t)(NH + 1) * 4, (void**)&tstart));
   ZK_TRY(ws.get("msm_bsums", ((std::max(len1, len2) + 1023) / 1024) * 4 + 16, (void**)&bsums));
   ZK_TRY(ws.get("msm_tot", 64, (void**)&tot));
-  ZK_HIP(hipEventRecord(lane->fork, ctx->stream));
-  ZK_HIP(hipStreamWaitEvent(st, lane->fork, 0));
+  if (ctx->msm_fork) {
+    ZK_HIP(hipStreamWaitEvent(st, ctx->msm_fork, 0));
+  } else {
+    ZK_HIP(hipEventRecord(lane->fork, ctx->stream));
+    ZK_HIP(hipStreamWaitEvent(st, lane->fork, 0));
+  }
   if ((debug_skip() & 1) && lane->debug_sorted) {
     *out_sval = sval;
     *out_bstart = bstart;
@@ -2729,7 +2800,11 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       ZK_HIP(hipGetLastError());
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);
-    k_msm_cutsum<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, L, buckets, xvalid, xpts, &flags[0]);
+    if (K <= CUTSUM_COOP_K)
+      k_msm_cutsum_coop<G><<<(unsigned)(((size_t)K * 16 + 255) / 256), 256, 0, st>>>(bstart, K, L, buckets, xvalid,
+                                                                                   xpts, &flags[0]);
+    else
+      k_msm_cutsum<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, L, buckets, xvalid, xpts, &flags[0]);
   }
   // segmented reduction of the remaining partials: level 1 pairs neighbours,
   // deeper levels only carry heavy buckets; each level exits on device when
@@ -2742,7 +2817,9 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
         set_error("msm: segmented reduction schedule too deep");
         return ZKMI_EINVAL;
       }
-      uint32_t Ll = level == 1 ? 2 : 16;
+      // small MSMs (latency-bound): 8 sequential additions per level, not 16
+      // (a level maps cur_len to 2 ceil(cur_len / Ll) + 1, so Ll >= 5 to shrink)
+      uint32_t Ll = level == 1 ? 2 : (K <= CUTSUM_COOP_K ? 8 : 16);
       uint32_t nc = (cur_len + Ll - 1) / Ll;
       k_msm_accN<G><<<(nc + 255) / 256, 256, 0, st>>>(xkey, xvalid, xpts, cur_len, Ll, nc, buckets, ykey, yvalid,
                                                       ypts, &flags[level - 1], &flags[level]);

@@ -164,6 +164,7 @@ void zkmi_ctx_destroy(zkmi_ctx* ctx) {
     delete l;
   }
   ctx->lanes.clear();
+  if (ctx->prove_fork) hipEventDestroy(ctx->prove_fork);
   for (auto& pb : ctx->pinned_free) hipHostFree(pb.first);
   ctx->pinned_free.clear();
   ctx->pinned_size.clear();

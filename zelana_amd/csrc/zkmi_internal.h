@@ -71,6 +71,10 @@ struct zkmi_ctx {
   int msm_lanes = 2;  // concurrent MSM streams
   int lane_next = 0;
   std::vector<zk::MsmLane*> lanes;
+  // set: MSM lanes wait on this event (recorded earlier on `stream`) instead
+  // of forking from the stream's current tail (groth16 small-proof schedule)
+  hipEvent_t msm_fork = nullptr;
+  hipEvent_t prove_fork = nullptr;  // owned: the event groth16_prove_submit uses for it
 };
 
 struct zkmi_bases {
