@@ -2209,6 +2209,7 @@ __global__ void __launch_bounds__(256) k_bases_negate(const uint32_t* __restrict
 }
 
 int bases_precompute(zkmi_bases* b, int c, int factor) {
+  graph_gen_bump();
   if (c < 4 || c > 22) {
     set_error("bases_precompute: window %d outside [4, 22]", c);
     return ZKMI_EINVAL;
@@ -2413,6 +2414,7 @@ struct zkmi_msm_job {
   zkmi_comm* comm = nullptr;    // sharded MSM: bit sums of every rank are summed
   size_t status_words = 0;      // sharded: status block after the bit sums (per rank)
   bool exchanged = false;       // sharded over RCCL: the data all-gather is queued
+  bool borrowed = false;        // graph replay: `host` belongs to the captured job
 };
 
 namespace zk {
@@ -2975,8 +2977,21 @@ void msm_job_free(zkmi_msm_job* job) {
     }
   }
   if (job->done) hipEventDestroy(job->done);
-  if (job->host) ctx_pinned_put(job->ctx, job->host);
+  if (job->host && !job->borrowed) ctx_pinned_put(job->ctx, job->host);
   delete job;
+}
+
+zkmi_msm_job* msm_job_replay(const zkmi_msm_job* cap, hipEvent_t done) {
+  zkmi_msm_job* j = new zkmi_msm_job(*cap);
+  j->done = done;
+  j->st = nullptr;  // its copy is finished by `done` (recorded after the graph launch)
+  j->borrowed = true;
+  return j;
+}
+void msm_job_release_captured(zkmi_msm_job* job) {
+  if (!job) return;
+  job->st = nullptr;  // the caller synchronised the context: no copy in flight
+  msm_job_free(job);
 }
 
 int msm_wait(zkmi_msm_job* job, uint64_t* out) {
