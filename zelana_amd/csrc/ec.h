@@ -213,23 +213,23 @@ ZK_HD Xyzz<FqOps> xyzz_mmadd_g1(const Aff<FqOps>& p, const Aff<FqOps>& q) {
 // Fq2 counterpart of xyzz_mmadd_g1 (four Fq2 products fewer than
 // xyzz_madd_g2).  In: p, q < 2p.  Out: as xyzz_madd_g2.
 ZK_HD Xyzz<Fq2Ops> xyzz_mmadd_g2(const Aff<Fq2Ops>& p, const Aff<Fq2Ops>& q) {
-  Fe2 pp_ = {subk<FqP, 2>(q.x.c0, p.x.c0), subk<FqP, 2>(q.x.c1, p.x.c1)};  // (0, 4p)
-  Fe2 rr = {subk<FqP, 2>(q.y.c0, p.y.c0), subk<FqP, 2>(q.y.c1, p.y.c1)};   // (0, 4p)
+  Fe2 pp_ = {subk<FqPn, 2>(q.x.c0, p.x.c0), subk<FqPn, 2>(q.x.c1, p.x.c1)};  // (0, 4p)
+  Fe2 rr = {subk<FqPn, 2>(q.y.c0, p.y.c0), subk<FqPn, 2>(q.y.c1, p.y.c1)};   // (0, 4p)
   Fe2 pp = f2_sqr_n(pp_);
   if (f2_is_zero(pp)) {
-    if (is_zero<FqP>(reduce8<FqP>(rr.c0)) && is_zero<FqP>(reduce8<FqP>(rr.c1))) return xyzz_mdbl(q);
+    if (is_zero<FqPn>(reduce8<FqPn>(rr.c0)) && is_zero<FqPn>(reduce8<FqPn>(rr.c1))) return xyzz_mdbl(q);
     return xyzz_inf<Fq2Ops>();
   }
   Fe2 r2 = f2_sqr_n(rr);
   Fe2 ppp = f2_mul_n(pp_, pp), qq = f2_mul_n(p.x, pp);
   Xyzz<Fq2Ops> r;
-  r.x.c0 = reduce8<FqP>(subk<FqP, 6>(r2.c0, add_lazy(add_lazy(ppp.c0, qq.c0), qq.c0)));
-  r.x.c1 = reduce8<FqP>(subk<FqP, 6>(r2.c1, add_lazy(add_lazy(ppp.c1, qq.c1), qq.c1)));
-  Fe2 qx = {subk<FqP, 2>(qq.c0, r.x.c0), subk<FqP, 2>(qq.c1, r.x.c1)};  // (0, 4p)
-  Fe ny0 = subk<FqP, 2>(fe_zero(), p.y.c0), ny1 = subk<FqP, 2>(fe_zero(), p.y.c1);
-  Fe nqx1 = subk<FqP, 4>(fe_zero(), qx.c1), nppp1 = subk<FqP, 2>(fe_zero(), ppp.c1);
-  r.y.c0 = mul4<FqP>(rr.c0, qx.c0, rr.c1, nqx1, ny0, ppp.c0, ny1, nppp1);
-  r.y.c1 = mul4<FqP>(rr.c0, qx.c1, rr.c1, qx.c0, ny0, ppp.c1, ny1, ppp.c0);
+  r.x.c0 = reduce8<FqPn>(subk<FqPn, 6>(r2.c0, add_lazy(add_lazy(ppp.c0, qq.c0), qq.c0)));
+  r.x.c1 = reduce8<FqPn>(subk<FqPn, 6>(r2.c1, add_lazy(add_lazy(ppp.c1, qq.c1), qq.c1)));
+  Fe2 qx = {subk<FqPn, 2>(qq.c0, r.x.c0), subk<FqPn, 2>(qq.c1, r.x.c1)};  // (0, 4p)
+  Fe ny0 = subk<FqPn, 2>(fe_zero(), p.y.c0), ny1 = subk<FqPn, 2>(fe_zero(), p.y.c1);
+  Fe nqx1 = subk<FqPn, 4>(fe_zero(), qx.c1), nppp1 = subk<FqPn, 2>(fe_zero(), ppp.c1);
+  r.y.c0 = mul4<FqPn>(rr.c0, qx.c0, rr.c1, nqx1, ny0, ppp.c0, ny1, nppp1);
+  r.y.c1 = mul4<FqPn>(rr.c0, qx.c1, rr.c1, qx.c0, ny0, ppp.c1, ny1, ppp.c0);
   r.zz = pp;
   r.zzz = ppp;
   return r;
@@ -241,23 +241,23 @@ ZK_HD Xyzz<Fq2Ops> xyzz_mmadd_g2(const Aff<Fq2Ops>& p, const Aff<Fq2Ops>& q) {
 ZK_HD Xyzz<Fq2Ops> xyzz_madd_g2(const Xyzz<Fq2Ops>& p, const Aff<Fq2Ops>& q) {
   if (xyzz_is_inf(p)) return xyzz_from_aff(q);
   Fe2 u2 = f2_mul_n(q.x, p.zz), s2 = f2_mul_n(q.y, p.zzz);
-  Fe2 pp_ = {subk<FqP, 2>(u2.c0, p.x.c0), subk<FqP, 2>(u2.c1, p.x.c1)};  // (0, 4p)
-  Fe2 rr = {subk<FqP, 2>(s2.c0, p.y.c0), subk<FqP, 2>(s2.c1, p.y.c1)};   // (0, 4p)
+  Fe2 pp_ = {subk<FqPn, 2>(u2.c0, p.x.c0), subk<FqPn, 2>(u2.c1, p.x.c1)};  // (0, 4p)
+  Fe2 rr = {subk<FqPn, 2>(s2.c0, p.y.c0), subk<FqPn, 2>(s2.c1, p.y.c1)};   // (0, 4p)
   Fe2 pp = f2_sqr_n(pp_);
   if (f2_is_zero(pp)) {
-    if (is_zero<FqP>(reduce8<FqP>(rr.c0)) && is_zero<FqP>(reduce8<FqP>(rr.c1))) return xyzz_mdbl(q);
+    if (is_zero<FqPn>(reduce8<FqPn>(rr.c0)) && is_zero<FqPn>(reduce8<FqPn>(rr.c1))) return xyzz_mdbl(q);
     return xyzz_inf<Fq2Ops>();
   }
   Fe2 r2 = f2_sqr_n(rr);
   Fe2 ppp = f2_mul_n(pp_, pp), qq = f2_mul_n(p.x, pp);
   Xyzz<Fq2Ops> r;
-  r.x.c0 = reduce8<FqP>(subk<FqP, 6>(r2.c0, add_lazy(add_lazy(ppp.c0, qq.c0), qq.c0)));
-  r.x.c1 = reduce8<FqP>(subk<FqP, 6>(r2.c1, add_lazy(add_lazy(ppp.c1, qq.c1), qq.c1)));
-  Fe2 qx = {subk<FqP, 2>(qq.c0, r.x.c0), subk<FqP, 2>(qq.c1, r.x.c1)};  // (0, 4p)
-  Fe ny0 = subk<FqP, 2>(fe_zero(), p.y.c0), ny1 = subk<FqP, 2>(fe_zero(), p.y.c1);
-  Fe nqx1 = subk<FqP, 4>(fe_zero(), qx.c1), nppp1 = subk<FqP, 2>(fe_zero(), ppp.c1);
-  r.y.c0 = mul4<FqP>(rr.c0, qx.c0, rr.c1, nqx1, ny0, ppp.c0, ny1, nppp1);
-  r.y.c1 = mul4<FqP>(rr.c0, qx.c1, rr.c1, qx.c0, ny0, ppp.c1, ny1, ppp.c0);
+  r.x.c0 = reduce8<FqPn>(subk<FqPn, 6>(r2.c0, add_lazy(add_lazy(ppp.c0, qq.c0), qq.c0)));
+  r.x.c1 = reduce8<FqPn>(subk<FqPn, 6>(r2.c1, add_lazy(add_lazy(ppp.c1, qq.c1), qq.c1)));
+  Fe2 qx = {subk<FqPn, 2>(qq.c0, r.x.c0), subk<FqPn, 2>(qq.c1, r.x.c1)};  // (0, 4p)
+  Fe ny0 = subk<FqPn, 2>(fe_zero(), p.y.c0), ny1 = subk<FqPn, 2>(fe_zero(), p.y.c1);
+  Fe nqx1 = subk<FqPn, 4>(fe_zero(), qx.c1), nppp1 = subk<FqPn, 2>(fe_zero(), ppp.c1);
+  r.y.c0 = mul4<FqPn>(rr.c0, qx.c0, rr.c1, nqx1, ny0, ppp.c0, ny1, nppp1);
+  r.y.c1 = mul4<FqPn>(rr.c0, qx.c1, rr.c1, qx.c0, ny0, ppp.c1, ny1, ppp.c0);
   r.zz = f2_mul_n(p.zz, pp);
   r.zzz = f2_mul_n(p.zzz, ppp);
   return r;
@@ -303,23 +303,23 @@ ZK_HD Xyzz<Fq2Ops> xyzz_add_g2(const Xyzz<Fq2Ops>& p, const Xyzz<Fq2Ops>& q) {
   if (xyzz_is_inf(q)) return p;
   Fe2 u1 = f2_mul_n(p.x, q.zz), u2 = f2_mul_n(q.x, p.zz);
   Fe2 s1 = f2_mul_n(p.y, q.zzz), s2 = f2_mul_n(q.y, p.zzz);
-  Fe2 pp_ = {subk<FqP, 2>(u2.c0, u1.c0), subk<FqP, 2>(u2.c1, u1.c1)};  // (0, 4p)
-  Fe2 rr = {subk<FqP, 2>(s2.c0, s1.c0), subk<FqP, 2>(s2.c1, s1.c1)};   // (0, 4p)
+  Fe2 pp_ = {subk<FqPn, 2>(u2.c0, u1.c0), subk<FqPn, 2>(u2.c1, u1.c1)};  // (0, 4p)
+  Fe2 rr = {subk<FqPn, 2>(s2.c0, s1.c0), subk<FqPn, 2>(s2.c1, s1.c1)};   // (0, 4p)
   Fe2 pp = f2_sqr_n(pp_);
   if (f2_is_zero(pp)) {
-    if (is_zero<FqP>(reduce8<FqP>(rr.c0)) && is_zero<FqP>(reduce8<FqP>(rr.c1))) return xyzz_dbl(p);
+    if (is_zero<FqPn>(reduce8<FqPn>(rr.c0)) && is_zero<FqPn>(reduce8<FqPn>(rr.c1))) return xyzz_dbl(p);
     return xyzz_inf<Fq2Ops>();
   }
   Fe2 r2 = f2_sqr_n(rr);
   Fe2 ppp = f2_mul_n(pp_, pp), qq = f2_mul_n(u1, pp);
   Xyzz<Fq2Ops> r;
-  r.x.c0 = reduce8<FqP>(subk<FqP, 6>(r2.c0, add_lazy(add_lazy(ppp.c0, qq.c0), qq.c0)));
-  r.x.c1 = reduce8<FqP>(subk<FqP, 6>(r2.c1, add_lazy(add_lazy(ppp.c1, qq.c1), qq.c1)));
-  Fe2 qx = {subk<FqP, 2>(qq.c0, r.x.c0), subk<FqP, 2>(qq.c1, r.x.c1)};  // (0, 4p)
-  Fe ny0 = subk<FqP, 2>(fe_zero(), s1.c0), ny1 = subk<FqP, 2>(fe_zero(), s1.c1);
-  Fe nqx1 = subk<FqP, 4>(fe_zero(), qx.c1), nppp1 = subk<FqP, 2>(fe_zero(), ppp.c1);
-  r.y.c0 = mul4<FqP>(rr.c0, qx.c0, rr.c1, nqx1, ny0, ppp.c0, ny1, nppp1);
-  r.y.c1 = mul4<FqP>(rr.c0, qx.c1, rr.c1, qx.c0, ny0, ppp.c1, ny1, ppp.c0);
+  r.x.c0 = reduce8<FqPn>(subk<FqPn, 6>(r2.c0, add_lazy(add_lazy(ppp.c0, qq.c0), qq.c0)));
+  r.x.c1 = reduce8<FqPn>(subk<FqPn, 6>(r2.c1, add_lazy(add_lazy(ppp.c1, qq.c1), qq.c1)));
+  Fe2 qx = {subk<FqPn, 2>(qq.c0, r.x.c0), subk<FqPn, 2>(qq.c1, r.x.c1)};  // (0, 4p)
+  Fe ny0 = subk<FqPn, 2>(fe_zero(), s1.c0), ny1 = subk<FqPn, 2>(fe_zero(), s1.c1);
+  Fe nqx1 = subk<FqPn, 4>(fe_zero(), qx.c1), nppp1 = subk<FqPn, 2>(fe_zero(), ppp.c1);
+  r.y.c0 = mul4<FqPn>(rr.c0, qx.c0, rr.c1, nqx1, ny0, ppp.c0, ny1, nppp1);
+  r.y.c1 = mul4<FqPn>(rr.c0, qx.c1, rr.c1, qx.c0, ny0, ppp.c1, ny1, ppp.c0);
   r.zz = f2_mul_n(f2_mul_n(p.zz, q.zz), pp);
   r.zzz = f2_mul_n(f2_mul_n(p.zzz, q.zzz), ppp);
   return r;

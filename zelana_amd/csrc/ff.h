@@ -34,6 +34,7 @@ struct Fe {
 
 // Base field q (G1/G2 coordinates)
 struct FqP {
+  static constexpr bool ASM = true;
   static constexpr uint32_t P[NL] = {0x187cfd47u, 0x010460b6u, 0x1c72a34fu, 0x02d522d0u, 0x1585d978u,
                                      0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
   static constexpr uint32_t P2[NL] = {0x10f9fa8eu, 0x0208c16du, 0x18e5469eu, 0x05aa45a1u, 0x0b0bb2f0u,
@@ -67,6 +68,7 @@ struct FqP {
 };
 // Scalar field r (NTT domain)
 struct FrP {
+  static constexpr bool ASM = true;
   static constexpr uint32_t P[NL] = {0x10000001u, 0x1f0fac9fu, 0x0e5c2450u, 0x07d090f3u, 0x1585d283u,
                                      0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
   static constexpr uint32_t P2[NL] = {0x00000002u, 0x1e1f593fu, 0x1cb848a1u, 0x0fa121e6u, 0x0b0ba506u,
@@ -85,6 +87,11 @@ struct FrP {
                                        0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};
   static constexpr uint32_t R2[NL] = {0x05b69bd4u, 0x06170a5au, 0x020cddceu, 0x1db6310bu, 0x0e54d0ffu,
                                       0x1cf855e3u, 0x1c15e103u, 0x07d09161u, 0x000a054au};
+};
+
+// Fq for G2 code: same constants, compiler-scheduled products (pmac)
+struct FqPn : FqP {
+  static constexpr bool ASM = false;
 };
 
 // ---------------------------------------------------------------- packing
@@ -168,6 +175,43 @@ ZK_HD void macs(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b;
 ZK_HD void mac1(uint64_t& acc, uint32_t d) { acc += d; }
 #endif
 
+// Product accumulation by field: P::ASM picks the one-chain inline-asm mads
+// (throughput kernels: G1, Fr) or plain C that the compiler may split into
+// parallel partial sums.  G2 (Fq2) code uses FqPn (ASM = false): at its 2
+// waves/SIMD the split chains win (2^20 G2 MSM, 2 lanes: 294 -> 308 Mpt/s),
+// and its ~half as many instructions (no hazard nops) fit the code in the
+// instruction cache.
+template <class P>
+ZK_HD void pmac(uint64_t& acc, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(ZK_NO_ASM_MAD)
+  if constexpr (P::ASM) {
+    mac(acc, a, b);
+    return;
+  }
+#endif
+  acc += (uint64_t)a * b;
+}
+template <class P>
+ZK_HD void pmacs(uint64_t& acc, uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(ZK_NO_ASM_MAD)
+  if constexpr (P::ASM) {
+    macs(acc, a, b);
+    return;
+  }
+#endif
+  acc += (uint64_t)a * b;
+}
+template <class P>
+ZK_HD void pmac1(uint64_t& acc, uint32_t d) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(ZK_NO_ASM_MAD)
+  if constexpr (P::ASM) {
+    mac1(acc, d);
+    return;
+  }
+#endif
+  acc += d;
+}
+
 // ------------------------------------------------------------ Montgomery mul
 // r = a*b*2^-261 mod p (lazy: result < 2p, normalised limbs).
 template <class P>
@@ -179,20 +223,20 @@ ZK_HD Fe mul(const Fe& a, const Fe& b) {
   for (int k = 0; k < NL; k++) {
 #pragma unroll
     for (int j = 0; j < k; j++) {
-      mac(acc, a.v[j], b.v[k - j]);
-      macs(acc, m[j], P::P[k - j]);
+      pmac<P>(acc, a.v[j], b.v[k - j]);
+      pmacs<P>(acc, m[j], P::P[k - j]);
     }
-    mac(acc, a.v[k], b.v[0]);
+    pmac<P>(acc, a.v[k], b.v[0]);
     m[k] = ((uint32_t)acc * P::PINV) & LMASK;
-    macs(acc, m[k], P::P[0]);
+    pmacs<P>(acc, m[k], P::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
 #pragma unroll
     for (int j = k - (NL - 1); j < NL; j++) {
-      mac(acc, a.v[j], b.v[k - j]);
-      macs(acc, m[j], P::P[k - j]);
+      pmac<P>(acc, a.v[j], b.v[k - j]);
+      pmacs<P>(acc, m[j], P::P[k - j]);
     }
     r.v[k - NL] = (uint32_t)acc & LMASK;
     acc >>= 29;
@@ -216,21 +260,21 @@ ZK_HD Fe mul_add(const Fe& a, const Fe& b, const Fe& d) {
   for (int k = 0; k < NL; k++) {
 #pragma unroll
     for (int j = 0; j < k; j++) {
-      mac(acc, a.v[j], b.v[k - j]);
-      macs(acc, m[j], P::P[k - j]);
+      pmac<P>(acc, a.v[j], b.v[k - j]);
+      pmacs<P>(acc, m[j], P::P[k - j]);
     }
-    mac(acc, a.v[k], b.v[0]);
+    pmac<P>(acc, a.v[k], b.v[0]);
     m[k] = ((uint32_t)acc * P::PINV) & LMASK;
-    macs(acc, m[k], P::P[0]);
+    pmacs<P>(acc, m[k], P::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
-    mac1(acc, d.v[k - NL]);
+    pmac1<P>(acc, d.v[k - NL]);
 #pragma unroll
     for (int j = k - (NL - 1); j < NL; j++) {
-      mac(acc, a.v[j], b.v[k - j]);
-      macs(acc, m[j], P::P[k - j]);
+      pmac<P>(acc, a.v[j], b.v[k - j]);
+      pmacs<P>(acc, m[j], P::P[k - j]);
     }
     r.v[k - NL] = (uint32_t)acc & LMASK;
     acc >>= 29;
@@ -249,22 +293,22 @@ ZK_HD Fe sqr_add(const Fe& a, const Fe& d) {
 #pragma unroll
   for (int k = 0; k < NL; k++) {
 #pragma unroll
-    for (int j = 0; j < (k + 1) / 2; j++) mac(acc, dd[j], a.v[k - j]);
-    if ((k & 1) == 0) mac(acc, a.v[k / 2], a.v[k / 2]);
+    for (int j = 0; j < (k + 1) / 2; j++) pmac<P>(acc, dd[j], a.v[k - j]);
+    if ((k & 1) == 0) pmac<P>(acc, a.v[k / 2], a.v[k / 2]);
 #pragma unroll
-    for (int j = 0; j < k; j++) macs(acc, m[j], P::P[k - j]);
+    for (int j = 0; j < k; j++) pmacs<P>(acc, m[j], P::P[k - j]);
     m[k] = ((uint32_t)acc * P::PINV) & LMASK;
-    macs(acc, m[k], P::P[0]);
+    pmacs<P>(acc, m[k], P::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
-    mac1(acc, d.v[k - NL]);
+    pmac1<P>(acc, d.v[k - NL]);
 #pragma unroll
-    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) mac(acc, dd[j], a.v[k - j]);
-    if ((k & 1) == 0) mac(acc, a.v[k / 2], a.v[k / 2]);
+    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) pmac<P>(acc, dd[j], a.v[k - j]);
+    if ((k & 1) == 0) pmac<P>(acc, a.v[k / 2], a.v[k / 2]);
 #pragma unroll
-    for (int j = k - (NL - 1); j < NL; j++) macs(acc, m[j], P::P[k - j]);
+    for (int j = k - (NL - 1); j < NL; j++) pmacs<P>(acc, m[j], P::P[k - j]);
     r.v[k - NL] = (uint32_t)acc & LMASK;
     acc >>= 29;
   }
@@ -304,21 +348,21 @@ ZK_HD Fe sqr(const Fe& a) {
 #pragma unroll
   for (int k = 0; k < NL; k++) {
 #pragma unroll
-    for (int j = 0; j < (k + 1) / 2; j++) mac(acc, d[j], a.v[k - j]);
-    if ((k & 1) == 0) mac(acc, a.v[k / 2], a.v[k / 2]);
+    for (int j = 0; j < (k + 1) / 2; j++) pmac<P>(acc, d[j], a.v[k - j]);
+    if ((k & 1) == 0) pmac<P>(acc, a.v[k / 2], a.v[k / 2]);
 #pragma unroll
-    for (int j = 0; j < k; j++) macs(acc, m[j], P::P[k - j]);
+    for (int j = 0; j < k; j++) pmacs<P>(acc, m[j], P::P[k - j]);
     m[k] = ((uint32_t)acc * P::PINV) & LMASK;
-    macs(acc, m[k], P::P[0]);
+    pmacs<P>(acc, m[k], P::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
 #pragma unroll
-    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) mac(acc, d[j], a.v[k - j]);
-    if ((k & 1) == 0) mac(acc, a.v[k / 2], a.v[k / 2]);
+    for (int j = k - (NL - 1); j < (k + 1) / 2; j++) pmac<P>(acc, d[j], a.v[k - j]);
+    if ((k & 1) == 0) pmac<P>(acc, a.v[k / 2], a.v[k / 2]);
 #pragma unroll
-    for (int j = k - (NL - 1); j < NL; j++) macs(acc, m[j], P::P[k - j]);
+    for (int j = k - (NL - 1); j < NL; j++) pmacs<P>(acc, m[j], P::P[k - j]);
     r.v[k - NL] = (uint32_t)acc & LMASK;
     acc >>= 29;
   }
@@ -419,23 +463,23 @@ ZK_HD Fe mul2(const Fe& a, const Fe& b, const Fe& c, const Fe& d) {
   for (int k = 0; k < NL; k++) {
 #pragma unroll
     for (int j = 0; j < k; j++) {
-      mac(acc, a.v[j], b.v[k - j]);
-      mac(acc, c.v[j], d.v[k - j]);
-      macs(acc, m[j], P::P[k - j]);
+      pmac<P>(acc, a.v[j], b.v[k - j]);
+      pmac<P>(acc, c.v[j], d.v[k - j]);
+      pmacs<P>(acc, m[j], P::P[k - j]);
     }
-    mac(acc, a.v[k], b.v[0]);
-    mac(acc, c.v[k], d.v[0]);
+    pmac<P>(acc, a.v[k], b.v[0]);
+    pmac<P>(acc, c.v[k], d.v[0]);
     m[k] = ((uint32_t)acc * P::PINV) & LMASK;
-    macs(acc, m[k], P::P[0]);
+    pmacs<P>(acc, m[k], P::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
 #pragma unroll
     for (int j = k - (NL - 1); j < NL; j++) {
-      mac(acc, a.v[j], b.v[k - j]);
-      mac(acc, c.v[j], d.v[k - j]);
-      macs(acc, m[j], P::P[k - j]);
+      pmac<P>(acc, a.v[j], b.v[k - j]);
+      pmac<P>(acc, c.v[j], d.v[k - j]);
+      pmacs<P>(acc, m[j], P::P[k - j]);
     }
     r.v[k - NL] = (uint32_t)acc & LMASK;
     acc >>= 29;
@@ -554,29 +598,29 @@ ZK_HD Fe mul4(const Fe& a, const Fe& b, const Fe& c, const Fe& d, const Fe& e, c
   for (int k = 0; k < NL; k++) {
 #pragma unroll
     for (int j = 0; j < k; j++) {
-      mac(acc, a.v[j], b.v[k - j]);
-      mac(acc, c.v[j], d.v[k - j]);
-      mac(acc, e.v[j], f.v[k - j]);
-      mac(acc, g.v[j], h.v[k - j]);
-      macs(acc, m[j], P::P[k - j]);
+      pmac<P>(acc, a.v[j], b.v[k - j]);
+      pmac<P>(acc, c.v[j], d.v[k - j]);
+      pmac<P>(acc, e.v[j], f.v[k - j]);
+      pmac<P>(acc, g.v[j], h.v[k - j]);
+      pmacs<P>(acc, m[j], P::P[k - j]);
     }
-    mac(acc, a.v[k], b.v[0]);
-    mac(acc, c.v[k], d.v[0]);
-    mac(acc, e.v[k], f.v[0]);
-    mac(acc, g.v[k], h.v[0]);
+    pmac<P>(acc, a.v[k], b.v[0]);
+    pmac<P>(acc, c.v[k], d.v[0]);
+    pmac<P>(acc, e.v[k], f.v[0]);
+    pmac<P>(acc, g.v[k], h.v[0]);
     m[k] = ((uint32_t)acc * P::PINV) & LMASK;
-    macs(acc, m[k], P::P[0]);
+    pmacs<P>(acc, m[k], P::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
 #pragma unroll
     for (int j = k - (NL - 1); j < NL; j++) {
-      mac(acc, a.v[j], b.v[k - j]);
-      mac(acc, c.v[j], d.v[k - j]);
-      mac(acc, e.v[j], f.v[k - j]);
-      mac(acc, g.v[j], h.v[k - j]);
-      macs(acc, m[j], P::P[k - j]);
+      pmac<P>(acc, a.v[j], b.v[k - j]);
+      pmac<P>(acc, c.v[j], d.v[k - j]);
+      pmac<P>(acc, e.v[j], f.v[k - j]);
+      pmac<P>(acc, g.v[j], h.v[k - j]);
+      pmacs<P>(acc, m[j], P::P[k - j]);
     }
     r.v[k - NL] = (uint32_t)acc & LMASK;
     acc >>= 29;
@@ -678,25 +722,25 @@ ZK_HD Fe pow(const Fe& a, const uint64_t e[4]) {
 struct Fe2 {
   Fe c0, c1;
 };
-ZK_HD Fe2 f2_add(const Fe2& a, const Fe2& b) { return {add<FqP>(a.c0, b.c0), add<FqP>(a.c1, b.c1)}; }
-ZK_HD Fe2 f2_sub(const Fe2& a, const Fe2& b) { return {sub<FqP>(a.c0, b.c0), sub<FqP>(a.c1, b.c1)}; }
-ZK_HD Fe2 f2_dbl(const Fe2& a) { return {dbl<FqP>(a.c0), dbl<FqP>(a.c1)}; }
-ZK_HD Fe2 f2_neg(const Fe2& a) { return {neg<FqP>(a.c0), neg<FqP>(a.c1)}; }
+ZK_HD Fe2 f2_add(const Fe2& a, const Fe2& b) { return {add<FqPn>(a.c0, b.c0), add<FqPn>(a.c1, b.c1)}; }
+ZK_HD Fe2 f2_sub(const Fe2& a, const Fe2& b) { return {sub<FqPn>(a.c0, b.c0), sub<FqPn>(a.c1, b.c1)}; }
+ZK_HD Fe2 f2_dbl(const Fe2& a) { return {dbl<FqPn>(a.c0), dbl<FqPn>(a.c1)}; }
+ZK_HD Fe2 f2_neg(const Fe2& a) { return {neg<FqPn>(a.c0), neg<FqPn>(a.c1)}; }
 ZK_HD Fe2 f2_mul(const Fe2& a, const Fe2& b) {
-  Fe t0 = mul<FqP>(a.c0, b.c0);
-  Fe t1 = mul<FqP>(a.c1, b.c1);
-  Fe t2 = mul<FqP>(add_lazy(a.c0, a.c1), add_lazy(b.c0, b.c1));
-  return {sub<FqP>(t0, t1), sub<FqP>(sub<FqP>(t2, t0), t1)};
+  Fe t0 = mul<FqPn>(a.c0, b.c0);
+  Fe t1 = mul<FqPn>(a.c1, b.c1);
+  Fe t2 = mul<FqPn>(add_lazy(a.c0, a.c1), add_lazy(b.c0, b.c1));
+  return {sub<FqPn>(t0, t1), sub<FqPn>(sub<FqPn>(t2, t0), t1)};
 }
 ZK_HD Fe2 f2_sqr(const Fe2& a) {
   // (a0 + a1 u)^2 = (a0+a1)(a0-a1) + 2 a0 a1 u
   Fe s = add_lazy(a.c0, a.c1);
-  Fe d = sub<FqP>(a.c0, a.c1);
-  Fe c0 = mul<FqP>(s, d);
-  Fe c1 = mul<FqP>(a.c0, a.c1);
-  return {c0, dbl<FqP>(c1)};
+  Fe d = sub<FqPn>(a.c0, a.c1);
+  Fe c0 = mul<FqPn>(s, d);
+  Fe c1 = mul<FqPn>(a.c0, a.c1);
+  return {c0, dbl<FqPn>(c1)};
 }
-ZK_HD bool f2_is_zero(const Fe2& a) { return is_zero<FqP>(a.c0) && is_zero<FqP>(a.c1); }
+ZK_HD bool f2_is_zero(const Fe2& a) { return is_zero<FqPn>(a.c0) && is_zero<FqPn>(a.c1); }
 ZK_HD bool fe_is_zero_raw(const Fe& a) {
   uint32_t o = 0;
 #pragma unroll
@@ -704,16 +748,16 @@ ZK_HD bool fe_is_zero_raw(const Fe& a) {
   return o == 0;
 }
 ZK_HD Fe2 f2_zero() { return {fe_zero(), fe_zero()}; }
-ZK_HD Fe2 f2_one() { return {one<FqP>(), fe_zero()}; }
+ZK_HD Fe2 f2_one() { return {one<FqPn>(), fe_zero()}; }
 
 // Fq2 products with one reduction per component (mul2): inputs normalised
 // limbs, values < 4p; outputs < 2p.
 ZK_HD Fe2 f2_mul_n(const Fe2& a, const Fe2& b) {
-  Fe nb1 = subk<FqP, 4>(fe_zero(), b.c1);
-  return {mul2<FqP>(a.c0, b.c0, a.c1, nb1), mul2<FqP>(a.c0, b.c1, a.c1, b.c0)};
+  Fe nb1 = subk<FqPn, 4>(fe_zero(), b.c1);
+  return {mul2<FqPn>(a.c0, b.c0, a.c1, nb1), mul2<FqPn>(a.c0, b.c1, a.c1, b.c0)};
 }
 ZK_HD Fe2 f2_sqr_n(const Fe2& a) {
-  return {mul<FqP>(add_lazy(a.c0, a.c1), subk<FqP, 4>(a.c0, a.c1)), mul<FqP>(add_lazy(a.c0, a.c0), a.c1)};
+  return {mul<FqPn>(add_lazy(a.c0, a.c1), subk<FqPn, 4>(a.c0, a.c1)), mul<FqPn>(add_lazy(a.c0, a.c0), a.c1)};
 }
 
 // Uniform field interface used by the curve templates.
