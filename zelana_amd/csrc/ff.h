@@ -67,8 +67,11 @@ struct FqP {
                                          0x3c908785u, 0x2684cc89u, 0x2f997e07u, 0x01e3eb0fu};
 };
 // Scalar field r (NTT domain)
+#ifndef ZK_FR_ASM
+#define ZK_FR_ASM 1
+#endif
 struct FrP {
-  static constexpr bool ASM = true;
+  static constexpr bool ASM = ZK_FR_ASM;
   static constexpr uint32_t P[NL] = {0x10000001u, 0x1f0fac9fu, 0x0e5c2450u, 0x07d090f3u, 0x1585d283u,
                                      0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
   static constexpr uint32_t P2[NL] = {0x00000002u, 0x1e1f593fu, 0x1cb848a1u, 0x0fa121e6u, 0x0b0ba506u,

@@ -270,7 +270,10 @@ __device__ __forceinline__ Fe ntt_tab_scale(Fe v, uint64_t i, const NttIo& io) {
 // to hide the load and twiddle latency the 2-wave form exposes).
 
 template <bool DIT, int PRO, int EPI, bool PERM, int TB, int RB>
-__global__ void __launch_bounds__(256, (RB == 3 ? 2 : 4)) k_ntt_group(const uint32_t* src, uint32_t* dst,
+#ifndef ZK_NTT_MINBLK
+#define ZK_NTT_MINBLK 4
+#endif
+__global__ void __launch_bounds__(256, (RB == 3 ? 2 : ZK_NTT_MINBLK)) k_ntt_group(const uint32_t* src, uint32_t* dst,
                                                                           const uint32_t* __restrict__ tw, uint32_t logn,
                                                                           uint32_t a, uint32_t k, NttIo io) {
   constexpr int TILE = 1 << TB, EPT = 1 << RB;
