@@ -156,3 +156,28 @@ def test_msm_table_linearity_and_sparse(ctx, log_n):
     ctx.set_window(16)
     assert np.array_equal(ctx.msm(bases, d), got)
     ctx.set_window(0)
+
+
+def test_msm_2pow20_table_plan_matches_oracle(ctx):
+    """Config 2 at its own size and plan: 2^20 uniform
+    scalars over the c = 20, 13-copy full table (one window of 13 x 2^20
+    entries, one lane per bucket), against the oracle's full 2^20 MSM
+    (ark-ec msm_bigint_wnaf restated) over the exported bases; also through
+    three lanes in flight, as the bench times it."""
+    import os
+    n = 1 << 20
+    bases = ctx.bases_generate(seed=1020, n=n)
+    info = bases.precompute()
+    assert info[1:] == (20, 13, 1), info  # the bench's headline plan
+    d = ctx.scalars_generate(seed=20, n=n)
+    hs = np.zeros((n, 4), np.uint64)
+    d.download(hs)
+    want = O.msm_g1(bases.export(), hs, threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(ctx.msm(bases, d), want)
+    ctx.set_lanes(3)
+    try:
+        jobs = [ctx.msm_submit(bases, d, n) for _ in range(3)]
+        for j in jobs:
+            assert np.array_equal(ctx.msm_wait(j), want)
+    finally:
+        ctx.set_lanes(2)

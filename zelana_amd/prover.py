@@ -124,6 +124,10 @@ class Groth16Prover:
         self.verifying_key = vk_bytes
         self.vk_hash = blake3(vk_bytes)
         self.circuit = circuit if circuit is not None else default_l2_synthesizer()
+        # per circuit shape: the recorded witness program, resident R1CS and
+        # z buffer (zp::Groth16Prover::prove's scheme; the C++ synthesizer
+        # records the program), used when the default synthesizer is
+        self._shapes: dict = {}
 
     @classmethod
     def from_bytes(cls, pk_bytes: bytes, vk_bytes: bytes, device: int = 0, circuit=None, compressed=True,
@@ -168,9 +172,39 @@ class Groth16Prover:
 
     # ---------------------------------------------------------- BatchProver
     def prove(self, inputs: BatchPublicInputs, witness) -> BatchProof:
-        """prover.rs:350-425: synthesize, r/s from StdRng(batch_id), prove on the GPU."""
-        cs, z = self.circuit(inputs, witness)
-        return self.prove_r1cs(cs, z, inputs)
+        """prover.rs:350-425: synthesize, r/s from StdRng(batch_id), prove on the GPU.
+
+        With the default (C++) synthesizer, the first batch of a circuit shape
+        is synthesized on the host, recording the shape's witness program;
+        later batches of that shape run the program on the GPU (z in HBM) and
+        prove it resident, as zp::Groth16Prover::prove does.  ZKMI_PY_SYNTH=1
+        or a custom `circuit` keeps per-call host synthesis."""
+        if self.circuit is not _native_synthesizer():
+            cs, z = self.circuit(inputs, witness)
+            return self.prove_r1cs(cs, z, inputs)
+        from . import host_prover as H
+        from .wprog import WitnessProgram
+        start = time.perf_counter()
+        key = H.l2_shape_key(inputs, witness)
+        sh = self._shapes.get(key)
+        if sh is None:
+            cs, z, plan = H.l2_record(inputs, witness)
+            sh = (plan, WitnessProgram(self.ctx, plan), gpu.R1CSDevice(self.ctx, cs),
+                  gpu.DeviceBuffer(self.ctx, plan.num_vars * 32))
+            if len(self._shapes) >= 8:
+                self._shapes.pop(next(iter(self._shapes)))
+            self._shapes[key] = sh
+            ins = plan.template_inputs
+        else:
+            ins = H.l2_witness_inputs(inputs, witness)
+        plan, wp, dev, dz = sh
+        rng = StdRng.seed_from_u64(inputs.batch_id)
+        r = rng.fr_rand()
+        s = rng.fr_rand()
+        wp.run(ins, dz)
+        a, b, c = gpu.groth16_prove_resident(self.ctx, self.pk, dev, dz, r, s)
+        return BatchProof(inputs, self.proof_to_solana_bytes(a, b, c),
+                          int((time.perf_counter() - start) * 1000), a, b, c)
 
     def prove_r1cs(self, cs, z, inputs: BatchPublicInputs) -> BatchProof:
         start = time.perf_counter()
@@ -233,6 +267,14 @@ def proof_points_from_solana_bytes(proof_bytes: bytes):
         y = _Q - y
         a[4:8] = [(y >> (64 * i)) & ((1 << 64) - 1) for i in range(4)]
     return a, b, c
+
+
+def _native_synthesizer():
+    try:
+        from .host_prover import native_l2_block_circuit
+        return native_l2_block_circuit
+    except ImportError:
+        return None
 
 
 def default_l2_synthesizer():
