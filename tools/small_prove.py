@@ -54,6 +54,17 @@ def main():
         t.append(time.perf_counter() - t0)
     out["resident_ms"] = [round(1e3 * float(np.median(t)), 3), round(1e3 * min(t), 3)]
     out["resident_proof"] = np.concatenate([np.asarray(x).ravel() for x in res]).tobytes().hex()[:16]
+    # host time to enqueue one proof (submit) against its end-to-end time
+    ts, tt = [], []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        job = gpu.groth16_prove_submit(ctx, pk, dev, dz, r, s)
+        t1 = time.perf_counter()
+        gpu.groth16_prove_wait(job)
+        ts.append(t1 - t0)
+        tt.append(time.perf_counter() - t0)
+    out["submit_host_ms"] = round(1e3 * float(np.median(ts)), 3)
+    out["submit_wait_ms"] = round(1e3 * float(np.median(tt)), 3)
     if os.environ.get("SP_RESIDENT_ONLY"):
         print(out, {k: v for k, v in os.environ.items() if k.startswith(("SP_", "ZKMI_"))}, flush=True)
         return

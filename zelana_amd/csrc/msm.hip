@@ -728,6 +728,24 @@ __device__ __forceinline__ Xyzz<F> shfl_xor_xyzz(const Xyzz<F>& a, int m) {
   r.zzz = shfl_xor_fe(a.zzz, m);
   return r;
 }
+__device__ __forceinline__ Fe shfl_down_fe(const Fe& a, uint32_t d) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = (uint32_t)__shfl_down((int)a.v[i], d, 16);
+  return r;
+}
+__device__ __forceinline__ Fe2 shfl_down_fe(const Fe2& a, uint32_t d) {
+  return {shfl_down_fe(a.c0, d), shfl_down_fe(a.c1, d)};
+}
+template <class F>
+__device__ __forceinline__ Xyzz<F> shfl_down_xyzz(const Xyzz<F>& a, uint32_t d) {
+  Xyzz<F> r;
+  r.x = shfl_down_fe(a.x, d);
+  r.y = shfl_down_fe(a.y, d);
+  r.zz = shfl_down_fe(a.zz, d);
+  r.zzz = shfl_down_fe(a.zzz, d);
+  return r;
+}
 constexpr uint32_t CUTSUM_COOP_K = 1u << 16;  // bucket counts up to which the tree form runs
 template <class G>
 __global__ void __launch_bounds__(256) k_msm_cutsum_coop(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t L,
@@ -1338,6 +1356,81 @@ __global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ x
   if (t == 0) {
     ykey[0] = first_key;
     yvalid[0] = 0;
+  }
+}
+
+// k_msm_accN for small MSMs (K <= CUTSUM_COOP_K, latency-bound): a chunk of
+// 16 partials is worked by 16 lanes, one partial each, and its key runs are
+// summed by a right-to-left segmented scan over lane shuffles (4 dependent
+// additions instead of 15); each run's head lane then writes it exactly as
+// the sequential kernel does (complete bucket, or the chunk's head / tail
+// slot for the next level).
+template <class G>
+__global__ void __launch_bounds__(256) k_msm_accN_coop(const uint32_t* __restrict__ xkey,
+                                                       const uint32_t* __restrict__ xvalid,
+                                                       const uint32_t* __restrict__ xpts, uint32_t M,
+                                                       uint32_t nchunks, uint32_t* __restrict__ buckets,
+                                                       uint32_t* __restrict__ ykey, uint32_t* __restrict__ yvalid,
+                                                       uint32_t* __restrict__ ypts,
+                                                       const uint32_t* __restrict__ prev_open,
+                                                       uint32_t* __restrict__ any_open) {
+  using F = typename G::F;
+  constexpr int XW = 4 * G::CW;
+  constexpr uint32_t L = 16;
+  const uint32_t gt = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t t = gt / L, r = gt % L;
+  if (*prev_open == 0) return;  // uniform over the launch
+  const bool chunk = t < nchunks;
+  const uint32_t start = t * L, end = chunk ? min(start + L, M) : 0;
+  const uint32_t p = start + r;
+  const bool in = chunk && p < end;
+  const uint32_t key = in ? xkey[p] : NOKEY - 1 - r;  // lanes past the end: distinct keys, no values
+  bool has = in && xvalid[p] != 0;
+  Xyzz<F> v = xyzz_inf<F>();
+  if (has) v = ld_xyzz<G>(xpts + (size_t)p * XW);
+#pragma unroll 1
+  for (uint32_t sft = 1; sft < L; sft <<= 1) {
+    const Xyzz<F> o = shfl_down_xyzz(v, sft);
+    const uint32_t ok = (uint32_t)__shfl_down((int)key, sft, L);
+    const bool oh = __shfl_down((int)has, sft, L) != 0;
+    if (r + sft < L && ok == key && oh) v = has ? br_add<G>(v, o) : o, has = true;
+  }
+  if (!chunk) return;
+  const uint32_t kprev = start > 0 ? xkey[start - 1] : NOKEY;
+  const uint32_t knext = end < M ? xkey[end] : NOKEY;
+  const uint32_t first_key = xkey[start], last_key = xkey[end - 1];
+  const uint32_t left = (uint32_t)__shfl_up((int)key, 1, L);
+  const bool head = in && (r == 0 || left != key);
+  // slots the chunk's head / tail runs did not fill (the sequential kernel's
+  // head_done / tail_done defaults): written first, by lane 0
+  const bool first_open = first_key == kprev, last_open = last_key == knext;
+  if (r == 0) {
+    if (!first_open) {
+      ykey[2 * t + 1] = first_key;
+      yvalid[2 * t + 1] = 0;
+    }
+    if (!last_open || (first_key == last_key && first_open)) {
+      ykey[2 * t + 2] = last_key;
+      yvalid[2 * t + 2] = 0;
+    }
+    if (t == 0) {
+      ykey[0] = first_key;
+      yvalid[0] = 0;
+    }
+  }
+  if (!head) return;
+  const bool left_open = r == 0 && first_open;
+  const bool right_open = key == last_key && last_open;
+  if (left_open || right_open) {
+    const uint32_t slot = left_open ? 2 * t + 1 : 2 * t + 2;
+    ykey[slot] = key;
+    yvalid[slot] = has;
+    if (has) {
+      st_xyzz<G>(ypts + (size_t)slot * XW, v);
+      atomicOr(any_open, 1u);
+    }
+  } else if (has) {
+    st_xyzz<G>(buckets + (size_t)key * XW, v);
   }
 }
 
@@ -2819,12 +2912,16 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
         set_error("msm: segmented reduction schedule too deep");
         return ZKMI_EINVAL;
       }
-      // small MSMs (latency-bound): 8 sequential additions per level, not 16
       // (a level maps cur_len to 2 ceil(cur_len / Ll) + 1, so Ll >= 5 to shrink)
-      uint32_t Ll = level == 1 ? 2 : (K <= CUTSUM_COOP_K ? 8 : 16);
+      const bool coop = level > 1 && K <= CUTSUM_COOP_K;  // small MSMs: 16-lane segmented scans
+      uint32_t Ll = level == 1 ? 2 : 16;
       uint32_t nc = (cur_len + Ll - 1) / Ll;
-      k_msm_accN<G><<<(nc + 255) / 256, 256, 0, st>>>(xkey, xvalid, xpts, cur_len, Ll, nc, buckets, ykey, yvalid,
-                                                      ypts, &flags[level - 1], &flags[level]);
+      if (coop)
+        k_msm_accN_coop<G><<<(unsigned)(((size_t)nc * 16 + 255) / 256), 256, 0, st>>>(
+            xkey, xvalid, xpts, cur_len, nc, buckets, ykey, yvalid, ypts, &flags[level - 1], &flags[level]);
+      else
+        k_msm_accN<G><<<(nc + 255) / 256, 256, 0, st>>>(xkey, xvalid, xpts, cur_len, Ll, nc, buckets, ykey, yvalid,
+                                                        ypts, &flags[level - 1], &flags[level]);
       std::swap(xkey, ykey);
       std::swap(xvalid, yvalid);
       std::swap(xpts, ypts);
