@@ -268,32 +268,33 @@ ZK_HD Xyzz<Fq2Ops> xyzz_madd_g2(const Xyzz<Fq2Ops>& p, const Aff<Fq2Ops>& q) {
 // brought back to [0, 2p) so the contract is xyzz_add's (the bucket
 // reductions store and exchange these points).  In/out: coordinates < 2p,
 // normalised.
+template <class P = FqP>
 ZK_HD Xyzz<FqOps> xyzz_add_g1(const Xyzz<FqOps>& p, const Xyzz<FqOps>& q) {
   if (xyzz_is_inf(p)) return q;
   if (xyzz_is_inf(q)) return p;
-  Fe u1 = mul<FqP>(p.x, q.zz);
-  Fe u2 = mul<FqP>(q.x, p.zz);
-  Fe s1 = mul<FqP>(p.y, q.zzz);
-  Fe s2 = mul<FqP>(q.y, p.zzz);
-  Fe pp_ = subk<FqP, 2>(u2, u1);          // U2 - U1 + 2p   in (0, 4p)
-  Fe ny1 = subk<FqP, 2>(fe_zero(), s1);   // 2p - S1        in (0, 2p]
+  Fe u1 = mul<P>(p.x, q.zz);
+  Fe u2 = mul<P>(q.x, p.zz);
+  Fe s1 = mul<P>(p.y, q.zzz);
+  Fe s2 = mul<P>(q.y, p.zzz);
+  Fe pp_ = subk<P, 2>(u2, u1);          // U2 - U1 + 2p   in (0, 4p)
+  Fe ny1 = subk<P, 2>(fe_zero(), s1);   // 2p - S1        in (0, 2p]
   Fe rr = add_lazy(s2, ny1);              // S2 - S1 + 2p   < 4p, limbs < 2^30
-  Fe pp = sqr<FqP>(pp_);
-  if (is_zero<FqP>(pp)) {
-    Fe rn = reduce8<FqP>(subk<FqP, 2>(s2, s1));
-    if (is_zero<FqP>(rn)) return xyzz_dbl(p);
+  Fe pp = sqr<P>(pp_);
+  if (is_zero<P>(pp)) {
+    Fe rn = reduce8<P>(subk<P, 2>(s2, s1));
+    if (is_zero<P>(rn)) return xyzz_dbl(p);
     return xyzz_inf<FqOps>();
   }
-  Fe ppp = mul<FqP>(pp_, pp);
-  Fe qq = mul<FqP>(u1, pp);
+  Fe ppp = mul<P>(pp_, pp);
+  Fe qq = mul<P>(u1, pp);
   Fe t = add_lazy(add_lazy(ppp, qq), qq);  // PPP + 2Q < 6p, limbs < 3*2^29
   Xyzz<FqOps> r;
-  Fe x = subk<FqP, 6>(sqr<FqP>(rr), t);    // in (0, 8p)
-  Fe qx = subk<FqP, 8>(qq, x);             // Q - X3 + 8p in (0, 10p)
-  r.y = mul2<FqP>(rr, qx, ny1, ppp);       // R (Q - X3) - S1 PPP
-  r.x = reduce8<FqP>(x);
-  r.zz = mul<FqP>(mul<FqP>(p.zz, q.zz), pp);
-  r.zzz = mul<FqP>(mul<FqP>(p.zzz, q.zzz), ppp);
+  Fe x = subk<P, 6>(sqr<P>(rr), t);    // in (0, 8p)
+  Fe qx = subk<P, 8>(qq, x);             // Q - X3 + 8p in (0, 10p)
+  r.y = mul2<P>(rr, qx, ny1, ppp);       // R (Q - X3) - S1 PPP
+  r.x = reduce8<P>(x);
+  r.zz = mul<P>(mul<P>(p.zz, q.zz), pp);
+  r.zzz = mul<P>(mul<P>(p.zzz, q.zzz), ppp);
   return r;
 }
 // Fq2 counterpart (the products of xyzz_madd_g2: one reduction per component).

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <string>
+#include <type_traits>
 #include <vector>
 #include <chrono>
 
@@ -43,11 +44,19 @@ namespace zk {
 // ----------------------------------------------------------------- traits
 struct G1T {
   using F = FqOps;
+  using P = FqP;                 // product form of the full additions (ff.h pmac)
   static constexpr int CW = 8;   // u32 words per coordinate
   static constexpr int PW = 16;  // u32 words per affine point
 };
+// G1 for the latency-bound kernels of small MSMs (cut sums, cascade, bucket
+// reduction below CUTSUM_COOP_K buckets): same layout, compiler-scheduled
+// products, whose split column chains shorten a lone wave's dependent path
+struct G1Tn : G1T {
+  using P = FqPn;
+};
 struct G2T {
   using F = Fq2Ops;
+  using P = FqPn;
   static constexpr int CW = 16;
   static constexpr int PW = 32;
 };
@@ -132,7 +141,7 @@ __device__ __forceinline__ void acc_step(Xyzz<typename G::F>& acc, bool& naff, c
 template <class G>
 __device__ __forceinline__ Xyzz<typename G::F> br_add(const Xyzz<typename G::F>& p, const Xyzz<typename G::F>& q) {
   if constexpr (ZK_BR_GENERIC) return xyzz_add(p, q);
-  else if constexpr (G::CW == 8) return xyzz_add_g1(p, q);
+  else if constexpr (G::CW == 8) return xyzz_add_g1<typename G::P>(p, q);
   else return xyzz_add_g2(p, q);
 }
 
@@ -2809,6 +2818,7 @@ template <class G>
 static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const zkmi_bases* tb, size_t offset,
                          size_t n, const uint32_t* sval, const uint32_t* bstart, zkmi_msm_job* job) {
   constexpr int XW = 4 * G::CW;
+  using GS = std::conditional_t<G::CW == 8, G1Tn, G>;  // the small-MSM kernels' trait
   hipStream_t st = lane->st;
   Workspace& ws = lane->ws;
   const uint32_t* d_bases = tb->d_pts + offset * G::PW;
@@ -2896,7 +2906,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);
     if (K <= CUTSUM_COOP_K)
-      k_msm_cutsum_coop<G><<<(unsigned)(((size_t)K * 16 + 255) / 256), 256, 0, st>>>(bstart, K, L, buckets, xvalid,
+      k_msm_cutsum_coop<GS><<<(unsigned)(((size_t)K * 16 + 255) / 256), 256, 0, st>>>(bstart, K, L, buckets, xvalid,
                                                                                    xpts, &flags[0]);
     else
       k_msm_cutsum<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, L, buckets, xvalid, xpts, &flags[0]);
@@ -2917,7 +2927,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       uint32_t Ll = level == 1 ? 2 : 16;
       uint32_t nc = (cur_len + Ll - 1) / Ll;
       if (coop)
-        k_msm_accN_coop<G><<<(unsigned)(((size_t)nc * 16 + 255) / 256), 256, 0, st>>>(
+        k_msm_accN_coop<GS><<<(unsigned)(((size_t)nc * 16 + 255) / 256), 256, 0, st>>>(
             xkey, xvalid, xpts, cur_len, nc, buckets, ykey, yvalid, ypts, &flags[level - 1], &flags[level]);
       else
         k_msm_accN<G><<<(nc + 255) / 256, 256, 0, st>>>(xkey, xvalid, xpts, cur_len, Ll, nc, buckets, ykey, yvalid,
@@ -2971,9 +2981,11 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       k_msm_br_strip<G><<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, bstart, lb, hb, W, sr, sc, bg.mc, Cb, Db);
     } else {
       uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc));
-      k_msm_br<G, false><<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, 256, Cb, Db);
+      auto br1 = K <= CUTSUM_COOP_K ? k_msm_br<GS, false> : k_msm_br<G, false>;
+      br1<<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, 256, Cb, Db);
     }
-    k_msm_br<G, true><<<(jobs2 + 3) / 4, 256, 0, brs>>>(Cb, Db, nullptr, lb, hb, W, sr, sc, sb, bg.segt, sums, nullptr);
+    auto br2 = K <= CUTSUM_COOP_K ? k_msm_br<GS, true> : k_msm_br<G, true>;
+    br2<<<(jobs2 + 3) / 4, 256, 0, brs>>>(Cb, Db, nullptr, lb, hb, W, sr, sc, sb, bg.segt, sums, nullptr);
     ZK_HIP(hipGetLastError());
   }
   job->sb = sb;
