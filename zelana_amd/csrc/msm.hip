@@ -2819,6 +2819,10 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
                          size_t n, const uint32_t* sval, const uint32_t* bstart, zkmi_msm_job* job) {
   constexpr int XW = 4 * G::CW;
   using GS = std::conditional_t<G::CW == 8, G1Tn, G>;  // the small-MSM kernels' trait
+#ifndef ZK_BR_N
+#define ZK_BR_N 0  // 1: the large-MSM bucket reductions with GS too (A/B)
+#endif
+  using GB = std::conditional_t<ZK_BR_N != 0, GS, G>;
   hipStream_t st = lane->st;
   Workspace& ws = lane->ws;
   const uint32_t* d_bases = tb->d_pts + offset * G::PW;
@@ -2876,7 +2880,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
                                                                xkey, xvalid, xpts);
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);
-    k_items_combine<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, buckets, xvalid, xpts, &nitems[1]);
+    k_items_combine<GB><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, buckets, xvalid, xpts, &nitems[1]);
     ZK_HIP(hipGetLastError());
   } else {
     // level 0: fixed-size chunks of the sorted list (sized from the upper bound
@@ -2978,13 +2982,13 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       const uint32_t nrow = (uint32_t)W * ((1u << hb) * sr), ncol = (uint32_t)W * ((1u << lb) * sc);
       const uint32_t cpw = 64u / (uint32_t)bg.mc;
       const uint32_t jobs1 = nrow + (ncol + cpw - 1) / cpw;
-      k_msm_br_strip<G><<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, bstart, lb, hb, W, sr, sc, bg.mc, Cb, Db);
+      k_msm_br_strip<GB><<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, bstart, lb, hb, W, sr, sc, bg.mc, Cb, Db);
     } else {
       uint32_t jobs1 = (uint32_t)W * (((1u << hb) * sr) + ((1u << lb) * sc));
       auto br1 = K <= CUTSUM_COOP_K ? k_msm_br<GS, false> : k_msm_br<G, false>;
       br1<<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, 256, Cb, Db);
     }
-    auto br2 = K <= CUTSUM_COOP_K ? k_msm_br<GS, true> : k_msm_br<G, true>;
+    auto br2 = K <= CUTSUM_COOP_K ? k_msm_br<GS, true> : k_msm_br<GB, true>;
     br2<<<(jobs2 + 3) / 4, 256, 0, brs>>>(Cb, Db, nullptr, lb, hb, W, sr, sc, sb, bg.segt, sums, nullptr);
     ZK_HIP(hipGetLastError());
   }
