@@ -15,7 +15,9 @@
 //     GPU, as on a 1-GPU box: RCCL refuses two ranks on one device);
 //   * RCCL: when dev0 != dev1 (the unique id travels over the pipe).
 // Cases: plain and fixed-base-table shards, a ragged total, an empty shard,
-// and window plans that differ between the ranks (must fail on both ranks).
+// window plans that differ between the ranks (must fail on both ranks), and
+// several MSMs in flight over one shard, whose plan is agreed once (host
+// transport: exactly one all-gather per MSM after the first).
 #include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -31,6 +33,7 @@ namespace {
 
 struct Link {
   int rank, wr, rd;
+  int calls = 0;  // host all-gathers issued (plan headers + bit-sum exchanges)
 };
 
 bool write_all(int fd, const void* p, size_t n) {
@@ -60,6 +63,7 @@ bool read_all(int fd, void* p, size_t n) {
 // first, so neither blocks on a full pipe.
 int pipe_allgather(void* user, const void* send, void* recv, size_t bytes) {
   Link* l = (Link*)user;
+  l->calls++;
   char* out = (char*)recv;
   memcpy(out + (size_t)l->rank * bytes, send, bytes);
   char* peer = out + (size_t)(1 - l->rank) * bytes;
@@ -113,6 +117,7 @@ int sharded_msm(zkmi_comm* comm, zkmi_ctx* ctx, int rank, uint64_t pseed, uint64
 }
 
 int run_rank(int rank, int dev, Link link, bool use_rccl) {
+  const int& link_calls = link.calls;
   zkmi_ctx* ctx = nullptr;
   if (zkmi_ctx_create(dev, &ctx)) {
     fprintf(stderr, "[rank %d] zkmi_ctx_create(%d): %s\n", rank, dev, zkmi_last_error());
@@ -152,6 +157,39 @@ int run_rank(int rank, int dev, Link link, bool use_rccl) {
     CHECK(full_msm(ctx, k.pseed, k.sseed, k.total, want), "full MSM total %zu", k.total);
     CHECK(memcmp(got, want, sizeof(got)) == 0, "sharded != global MSM (total %zu, table %d)", k.total, (int)k.table);
     if (rank == 0) printf("case total=%zu table=%d: %s\n", k.total, (int)k.table, memcmp(got, want, 64) ? "MISMATCH" : "ok");
+  }
+  // one shard, several MSMs in flight: the window plan is agreed by the first
+  // submit only (later submits run no control collective); pinning another
+  // window on both ranks agrees a new plan
+  {
+    const size_t total = (1u << 17) + 5;
+    size_t first = 0, count = 0;
+    zkmi_shard_range(total, 2, rank, &first, &count);
+    zkmi_bases* b = nullptr;
+    void* d = nullptr;
+    CHECK(zkmi_bases_generate_range_g1(ctx, 21, first, count, &b) == 0 &&
+              zkmi_dev_alloc(ctx, count * 32 + 32, &d) == 0 &&
+              zkmi_scalars_generate_range(ctx, 22, first, count, d) == 0,
+          "inputs");
+    uint64_t want[8] = {0};
+    CHECK(full_msm(ctx, 21, 22, total, want), "full MSM");
+    for (int win : {0, 13}) {
+      CHECK(zkmi_msm_set_window(ctx, win) == 0, "set window %d", win);
+      const int calls0 = link_calls;
+      zkmi_msm_job* jobs[3] = {nullptr, nullptr, nullptr};
+      for (auto& j : jobs) CHECK(zkmi_msm_sharded_submit(comm, b, 0, d, count, &j) == 0, "submit");
+      for (auto& j : jobs) {
+        uint64_t got[8] = {0};
+        CHECK(j && zkmi_msm_wait(j, got) == 0 && memcmp(got, want, sizeof(got)) == 0,
+              "cached-plan sharded MSM (window %d) != global", win);
+      }
+      if (!use_rccl)  // one header exchange + three bit-sum exchanges
+        CHECK(link_calls - calls0 == 4, "window %d: %d host all-gathers for 3 MSMs", win, link_calls - calls0);
+    }
+    CHECK(zkmi_msm_set_window(ctx, 0) == 0, "set window 0");
+    zkmi_dev_free(ctx, d);
+    zkmi_bases_destroy(b);
+    if (rank == 0) printf("cached plan: ok\n");
   }
   // different window plans on the two ranks must fail on BOTH ranks
   {

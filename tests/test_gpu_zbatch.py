@@ -175,3 +175,37 @@ def test_gpu_witness_program_full(ctx):
         for g, w in zip(o, want[k]):
             assert np.array_equal(g, w)
     wp.close()
+
+
+def test_batch_worker_generate_batch_proof(ctx):
+    """zelana_amd.batch_worker.ZBatchProver (the forge worker's
+    generate_batch_proof surface, prover-worker/src/prover.rs:454-565) on a
+    reduced circuit: GPU witness + resident prove equal the host-built z and
+    the oracle's proof under the same key, r, s; the proof verifies (pairing)
+    with the public inputs the ProofResult carries, in the worker's layout."""
+    from zelana_amd import batch_worker as BW
+    from zelana_amd import gpu
+    from zelana_amd.rng import StdRng
+    import pairing as PR
+    shape = dict(max_transfers=1, max_withdrawals=1, max_shielded=1, depth=2)
+    d = Z.synthetic_batch(2, 1, seed=102)
+    cs, z, _ = Z.build(d, **shape)
+    st, keep = O.make_r1cs(cs)
+    opk = O.lib().oracle_groth16_setup(ctypes.byref(st), O.Rng(0).h, 8)
+    size = O.lib().oracle_pk_serialize(opk, 1, None, 0)
+    buf = np.zeros(size, np.uint8)
+    O.lib().oracle_pk_serialize(opk, 1, buf.ctypes.data, size)
+    w = BW.ZBatchProver(ctx, d, pk=gpu.ProvingKey(ctx, buf.tobytes(), True), **shape)
+    res = w.generate_batch_proof(d)
+    assert np.array_equal(w.witness(), z)
+    prs = StdRng.seed_from_u64(int(d["batch_id"]))
+    r, s = prs.fr_rand(), prs.fr_rand()
+    want = _oracle_prove(opk, st, z, r, s)
+    assert res.proof_bytes == gpu.proof_to_solana_bytes(*want)
+    assert res.proof == res.proof_bytes.hex() and len(res.proof_bytes) == 256
+    pub = [int(h, 16) for h in res.public_inputs]
+    assert pub == [O.limbs_to_int(z[i]) for i in range(1, cs.num_instance)]
+    assert len(res.public_witness_bytes) == 12 + 32 * 7
+    assert PR.verify_with_oracle_vk(opk, cs.num_instance, pub, *want)
+    w.close()
+    O.lib().oracle_pk_free(opk)

@@ -16,6 +16,7 @@
 // the same lane with no host round trip.
 #include <string.h>
 
+#include <atomic>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -108,8 +109,10 @@ static int comm_new(zkmi_ctx* ctx, int nranks, int rank, int kind, zkmi_comm** o
     set_error("zkmi_comm_init: bad arguments (nranks %d, rank %d)", nranks, rank);
     return ZKMI_EINVAL;
   }
+  static std::atomic<uint64_t> next_serial{1};
   zkmi_comm* c = new zkmi_comm;
   c->ctx = ctx;
+  c->serial = next_serial++;
   c->nranks = nranks;
   c->rank = rank;
   c->kind = kind;

@@ -233,22 +233,49 @@ __global__ void __launch_bounds__(256) k_to_mont_fr(const uint32_t* __restrict__
 // rows i < m: out[i] = sum_k val_k * z[col_k]  (val canonical, z Montgomery ->
 // canonical product); rows m <= i < m + l of A copy z (inputs appended to A
 // only); the rest of the domain is zero.  (evaluate_constraint, §8a a5)
+// A wave owns 64 consecutive rows.  Rows of at most MATVEC_SHORT terms are
+// summed by their own lane; longer rows (Poseidon/packing rows, 254-term bit
+// recompositions) are summed by the whole wave in turn -- lanes stride over
+// the row's terms, then a 6-level shuffle tree -- so one long row no longer
+// serialises in one lane (config 1's C mat-vec: 262 us one lane per row).
+constexpr uint32_t MATVEC_SHORT = 8;
+__device__ __forceinline__ Fe fe_shfl_xor(const Fe& a, int m) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], m, 64);
+  return r;
+}
 __global__ void __launch_bounds__(256) k_matvec(const uint64_t* __restrict__ rowptr, const uint64_t* __restrict__ col,
                                                 const uint32_t* __restrict__ val, const uint32_t* __restrict__ zm,
                                                 const uint32_t* __restrict__ zc, size_t m, size_t l, size_t n,
                                                 int is_a, uint32_t* __restrict__ out) {
-  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // lanes past n join the shuffles
+  const int lane = threadIdx.x & 63;
   Fe acc = fe_zero();
+  uint64_t k0 = 0, k1 = 0;
   if (i < m) {
-    for (uint64_t k = rowptr[i]; k < rowptr[i + 1]; k++) {
-      Fe t = mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8));
-      acc = add<FrP>(acc, t);
-    }
-  } else if (is_a && i < m + l) {
+    k0 = rowptr[i];
+    k1 = rowptr[i + 1];
+  }
+  const bool longrow = k1 - k0 > MATVEC_SHORT;
+  if (i < m && !longrow) {
+    for (uint64_t k = k0; k < k1; k++) acc = add<FrP>(acc, mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8)));
+  } else if (is_a && i >= m && i < m + l) {
     acc = ld_fe(zc + (i - m) * 8);
   }
-  st_fe(out + i * 8, acc);
+  uint64_t pending = __ballot(longrow);  // wave-uniform
+  while (pending) {
+    const int src = __builtin_ctzll(pending);
+    pending &= pending - 1;
+    const uint64_t b0 = __shfl(k0, src, 64), b1 = __shfl(k1, src, 64);
+    Fe part = fe_zero();
+    for (uint64_t k = b0 + lane; k < b1; k += 64)
+      part = add<FrP>(part, mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8)));
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) part = add<FrP>(part, fe_shfl_xor(part, d));
+    if (lane == src) acc = part;
+  }
+  if (i < n) st_fe(out + i * 8, acc);
 }
 // powers table: tab[x] = c * base^(x * step) for x < cnt (Montgomery), runs of 64
 __global__ void __launch_bounds__(256) k_pow_table(uint32_t* __restrict__ tab, uint32_t cnt, const uint32_t* base_c,

@@ -41,6 +41,21 @@
 
 namespace zk {
 
+// Wave priority of the pipeline's tail kernels (sort, scans, item plan,
+// piece sums, bucket reduction).  With several MSM lanes in flight they share
+// SIMDs with another lane's accumulation, whose older waves win the
+// oldest-first issue arbitration: in a rocprofv3 trace of the 3-lane 2^20
+// pipeline the 12-us P1 count took 462 us and the scans 7 -> 48 us, and no
+// accumulation ran for 28% of the step.  The tails issue little VALU work, so
+// letting them win arbitration costs the accumulation little.
+#ifndef ZK_TAIL_PRIO
+#define ZK_TAIL_PRIO 3
+#endif
+#define ZK_TAIL_WAVE()                                        \
+  do {                                                        \
+    if (ZK_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(ZK_TAIL_PRIO); \
+  } while (0)
+
 // ----------------------------------------------------------------- traits
 struct G1T {
   using F = FqOps;
@@ -204,6 +219,7 @@ __device__ __forceinline__ void scalar_digits(const uint32_t* __restrict__ scala
 template <int C, bool BAL>
 __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars, size_t n, int p, int Wp,
                                                     int32_t* __restrict__ digits) {
+  ZK_TAIL_WAVE();
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   constexpr int W = msm_windows(C);
@@ -263,6 +279,7 @@ __device__ __forceinline__ bool rs_key(const int32_t* __restrict__ digits, uint6
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_count(const int32_t* __restrict__ digits, uint64_t M, uint32_t ne,
                                                             uint32_t B, uint32_t NH, uint32_t lob, uint32_t C1,
                                                             uint32_t nc1, uint32_t* __restrict__ cnt1) {
+  ZK_TAIL_WAVE();
   extern __shared__ uint32_t hist[];
   for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) hist[x] = 0;
   __syncthreads();
@@ -398,6 +415,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_scatter(const int32_t* __r
                                                               uint32_t ne, uint32_t B, uint32_t NH, uint32_t lob,
                                                               uint32_t C1, uint32_t nc1, const uint32_t* __restrict__ offs1,
                                                               uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+  ZK_TAIL_WAVE();
   extern __shared__ uint32_t lds[];
   for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) lds[2 * NH + x] = offs1[(size_t)x * nc1 + blockIdx.x];
   const uint64_t base = (uint64_t)blockIdx.x * C1;
@@ -436,6 +454,7 @@ template <int C, bool BAL>
 __global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_count(const uint32_t* __restrict__ scalars, size_t n, int Wp,
                                                              uint32_t B, uint32_t NH, uint32_t lob, uint32_t CS,
                                                              uint32_t nc1, uint32_t* __restrict__ cnt1) {
+  ZK_TAIL_WAVE();
   extern __shared__ uint32_t hist[];
   constexpr int W = msm_windows(C);
   for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) hist[x] = 0;
@@ -460,6 +479,7 @@ __global__ void __launch_bounds__(T) k_rs_p1f_scatter(const uint32_t* __restrict
                                                                uint32_t B, uint32_t NH, uint32_t lob, uint32_t CS,
                                                                uint32_t nc1, const uint32_t* __restrict__ offs1,
                                                                uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+  ZK_TAIL_WAVE();
   extern __shared__ uint32_t lds[];
   constexpr int W = msm_windows(C);
   for (uint32_t x = threadIdx.x; x < NH; x += T) lds[2 * NH + x] = offs1[(size_t)x * nc1 + blockIdx.x];
@@ -483,6 +503,7 @@ __global__ void __launch_bounds__(T) k_rs_p1f_scatter(const uint32_t* __restrict
 __global__ void __launch_bounds__(1024) k_rs_tiles(const uint32_t* __restrict__ offs1, uint32_t nc1, uint32_t NH,
                                                    const uint32_t* __restrict__ total, uint32_t C2,
                                                    uint32_t* __restrict__ binstart, uint32_t* __restrict__ tstart) {
+  ZK_TAIL_WAVE();
   __shared__ uint32_t sh[1024];
   const uint32_t tot = *total;
   uint32_t carry = 0;
@@ -537,6 +558,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p2_count(const uint32_t* __re
                                                             const uint32_t* __restrict__ tstart, uint32_t NH,
                                                             uint32_t lob, uint32_t C2, uint32_t T2max,
                                                             uint32_t* __restrict__ cnt2) {
+  ZK_TAIL_WAVE();
   extern __shared__ uint32_t hist[];
   const uint32_t NLO = 1u << lob, mask = NLO - 1;
   const uint32_t t = rs_xcd_tile(blockIdx.x, T2max);
@@ -570,6 +592,7 @@ __global__ void __launch_bounds__(T) k_rs_p2_scatter(const uint32_t* __restrict_
                                                               uint32_t lob, uint32_t C2, uint32_t T2max,
                                                               const uint32_t* __restrict__ offs2,
                                                               uint32_t* __restrict__ sval) {
+  ZK_TAIL_WAVE();
   extern __shared__ uint32_t lds[];
   const uint32_t NLO = 1u << lob, mask = NLO - 1;
   const uint32_t t = rs_xcd_tile(blockIdx.x, T2max);
@@ -592,6 +615,7 @@ __global__ void __launch_bounds__(256) k_rs_bstart(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ binstart,
                                                    const uint32_t* __restrict__ tstart, uint32_t NH, uint32_t lob,
                                                    uint32_t K, uint32_t* __restrict__ bstart) {
+  ZK_TAIL_WAVE();
   uint32_t k = blockIdx.x * 256 + threadIdx.x;
   if (k > K) return;
   if (k == K) {
@@ -606,6 +630,7 @@ __global__ void __launch_bounds__(256) k_rs_bstart(const uint32_t* __restrict__ 
 // exclusive scan of counts[K] -> offs[K+1]; 1024 elements per block
 __global__ void __launch_bounds__(256) k_scan_blocks(const uint32_t* in, uint32_t K, uint32_t* out,
                                                      uint32_t* __restrict__ block_sums) {
+  ZK_TAIL_WAVE();
   __shared__ uint32_t sh[256];
   uint32_t base = blockIdx.x * 1024 + threadIdx.x * 4;
   uint32_t v[4], s = 0;
@@ -632,6 +657,7 @@ __global__ void __launch_bounds__(256) k_scan_blocks(const uint32_t* in, uint32_
 }
 // single block: exclusive scan of block sums in place (any length)
 __global__ void __launch_bounds__(1024) k_scan_top(uint32_t* __restrict__ bs, uint32_t nb, uint32_t* __restrict__ total) {
+  ZK_TAIL_WAVE();
   __shared__ uint32_t sh[1024];
   uint32_t carry = 0;
   for (uint32_t base = 0; base < nb; base += 1024) {
@@ -654,6 +680,7 @@ __global__ void __launch_bounds__(1024) k_scan_top(uint32_t* __restrict__ bs, ui
 }
 __global__ void __launch_bounds__(256) k_scan_add(uint32_t* __restrict__ out, uint32_t K,
                                                   const uint32_t* __restrict__ bs, uint32_t* __restrict__ cursor) {
+  ZK_TAIL_WAVE();
   uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= K) return;
   uint32_t v = out[i] + bs[i / 1024];
@@ -693,6 +720,7 @@ __global__ void __launch_bounds__(256) k_msm_cutsum(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ buckets, uint32_t* __restrict__ xvalid,
                                                     const uint32_t* __restrict__ xpts,
                                                     uint32_t* __restrict__ open_flag) {
+  ZK_TAIL_WAVE();
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -762,6 +790,7 @@ __global__ void __launch_bounds__(256) k_msm_cutsum_coop(const uint32_t* __restr
                                                          uint32_t* __restrict__ xvalid,
                                                          const uint32_t* __restrict__ xpts,
                                                          uint32_t* __restrict__ open_flag) {
+  ZK_TAIL_WAVE();
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   const uint32_t gt = blockIdx.x * 256 + threadIdx.x;
@@ -1009,6 +1038,7 @@ constexpr uint32_t ITEMS_IPT = 8;
 __global__ void __launch_bounds__(256) k_items_count(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
                                                      uint32_t* __restrict__ hist, uint32_t* __restrict__ hv,
                                                      uint32_t* __restrict__ open_flag) {
+  ZK_TAIL_WAVE();
   __shared__ uint32_t lh[ITEM_CAP_MAX + 1];
   for (uint32_t i = threadIdx.x; i <= cap; i += 256) lh[i] = 0;
   __syncthreads();
@@ -1036,12 +1066,14 @@ __global__ void __launch_bounds__(256) k_items_count(const uint32_t* __restrict_
 // one thread: cursors of the size classes, longest class first; total items
 __global__ void k_items_offsets(const uint32_t* __restrict__ hist, uint32_t cap, uint32_t* __restrict__ cursor,
                                 uint32_t* __restrict__ nitems) {
+  ZK_TAIL_WAVE();
   uint32_t run = 0;
   for (uint32_t cl = cap; cl >= 1; cl--) {
     cursor[cl] = run;
     run += hist[cl];
   }
-  *nitems = run;
+  nitems[0] = run;
+  nitems[2] = 0;  // work counter of the persistent accumulation (k_acc_items_g1p)
 }
 
 // Also resets the partial list the segmented cascade reads (xkey = no key,
@@ -1052,6 +1084,7 @@ __global__ void __launch_bounds__(256) k_items_scatter(const uint32_t* __restric
                                                        uint32_t* __restrict__ cursor, uint4* __restrict__ items,
                                                        const uint32_t* __restrict__ open_flag, uint32_t* __restrict__ xkey,
                                                        uint32_t* __restrict__ xvalid, uint32_t xl) {
+  ZK_TAIL_WAVE();
   if (*open_flag) {
     for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < xl; i += (size_t)gridDim.x * 256) {
       xkey[i] = 0xFFFFFFFFu;
@@ -1179,10 +1212,10 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
                                               const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
                                               const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
                                               uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey,
-                                              uint32_t* __restrict__ xvalid, uint32_t* __restrict__ xpts) {
+                                              uint32_t* __restrict__ xvalid, uint32_t* __restrict__ xpts,
+                                              uint32_t i) {
   using F = FqOps;
   constexpr int XW = 32;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= *nitems) return;
   const uint4 it = items[i];
   const uint32_t start = it.x, end = it.y;
@@ -1259,7 +1292,29 @@ __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                    uint32_t* __restrict__ xpts) {
   if constexpr (ZK_ACC_G1_V1) acc_items_body<G1T>(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts);
-  else acc_items_g1f(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts);
+  else acc_items_g1f(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts,
+                     blockIdx.x * blockDim.x + threadIdx.x);
+}
+// Persistent form: a grid of a few workgroups per CU whose waves take 64
+// items at a time from a counter (nitems[2], reset by k_items_offsets), in the
+// plan's longest-first order.  Launched with fewer waves per SIMD than the
+// kernel's VGPR budget allows, it leaves room for other lanes' sort and
+// bucket-reduction waves to run beside it.
+__global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
+    k_acc_items_g1p(const uint4* __restrict__ items, uint32_t* __restrict__ nitems,
+                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
+                    const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
+                    uint32_t* __restrict__ xpts) {
+  const uint32_t total = nitems[0];
+  const int lane = threadIdx.x & 63;
+  for (;;) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&nitems[2], 64u);
+    base = (uint32_t)__shfl((int)base, 0, 64);
+    if (base >= total) break;
+    acc_items_g1f(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts, base + lane);
+  }
 }
 __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
     k_acc_items_g2(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
@@ -1278,6 +1333,7 @@ __global__ void __launch_bounds__(256) k_items_combine(const uint32_t* __restric
                                                        uint32_t* __restrict__ buckets, uint32_t* __restrict__ xvalid,
                                                        const uint32_t* __restrict__ xpts,
                                                        const uint32_t* __restrict__ npieces) {
+  ZK_TAIL_WAVE();
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   const uint32_t b = blockIdx.x * 256 + threadIdx.x;
@@ -1302,6 +1358,7 @@ __global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ x
                                                   uint32_t* __restrict__ ykey, uint32_t* __restrict__ yvalid,
                                                   uint32_t* __restrict__ ypts, const uint32_t* __restrict__ prev_open,
                                                   uint32_t* __restrict__ any_open) {
+  ZK_TAIL_WAVE();
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1383,6 +1440,7 @@ __global__ void __launch_bounds__(256) k_msm_accN_coop(const uint32_t* __restric
                                                        uint32_t* __restrict__ ypts,
                                                        const uint32_t* __restrict__ prev_open,
                                                        uint32_t* __restrict__ any_open) {
+  ZK_TAIL_WAVE();
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   constexpr uint32_t L = 16;
@@ -1466,6 +1524,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
                                                 const uint32_t* __restrict__ bstart, int lb, int hb, int W, int sr,
                                                 int sc, int sb, int segt, uint32_t* __restrict__ out0,
                                                 uint32_t* __restrict__ out1) {
+  ZK_TAIL_WAVE();
   // Rows and columns are cut into sr / sc segments of <= 256 buckets, one wave
   // each (enough waves for 2^19-bucket windows); C[h][seg], D[l][seg].  Bit
   // sums are cut into sb segments of segt (64..256) terms; the host adds
@@ -1578,6 +1637,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
                                                       const uint32_t* __restrict__ bstart, int lb, int hb, int W,
                                                       int sr, int sc, int mc, uint32_t* __restrict__ outC,
                                                       uint32_t* __restrict__ outD) {
+  ZK_TAIL_WAVE();
   // mc = lanes per column line (a power of two <= 64): 64 / mc columns share
   // a wave, so a short column gets the same fold length as a row and a
   // shallower tree (2^19 buckets: 512-bucket columns, mc = 32 -> 16 folds +
@@ -2785,13 +2845,22 @@ static BrGeom br_geom(const MsmPlan& P, bool g2) {
 // u32 at d_sums) on stream st (the lane stream): for a sharded MSM over RCCL, first the
 // all-gather of every rank's bit sums (comm stream, ordered after the lane's
 // work), then the D2H into the job's pinned buffer and the job's event.
+// Plan signature word of a sharded job's status block (with sb and W).
+static uint32_t shard_sig0(const zkmi_msm_job* job) {
+  return 0x5A000000u | ((uint32_t)job->g2 << 16) | ((uint32_t)job->c << 8) | (uint32_t)job->bb;
+}
+
 static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, hipStream_t st, zkmi_msm_job* job, const uint32_t* d_sums,
                               size_t words) {
   const int nr = job->comm ? job->comm->nranks : 1;
   const bool dev_gather = job->comm && job->comm->kind == ZKMI_COMM_RCCL;
   const uint32_t* src = d_sums;
-  if (job->comm) {  // sharded: a zero status block ends this rank's payload (d_sums has room)
-    ZK_HIP(hipMemsetAsync(const_cast<uint32_t*>(d_sums) + words, 0, SHARD_STATUS_WORDS * 4, st));
+  if (job->comm) {  // sharded: a status block ends this rank's payload (d_sums has room):
+    // word 0 = failure flag (0 here), words 1..3 = the plan signature msm_wait compares
+    uint32_t* stw = const_cast<uint32_t*>(d_sums) + words;
+    const uint32_t sig[3] = {shard_sig0(job), (uint32_t)job->sb, (uint32_t)job->W};
+    ZK_HIP(hipMemsetAsync(stw, 0, 4, st));
+    for (int i = 0; i < 3; i++) ZK_HIP(hipMemsetD32Async((hipDeviceptr_t)(stw + 1 + i), (int)sig[i], 1, st));
     words += SHARD_STATUS_WORDS;
     job->status_words = SHARD_STATUS_WORDS;
   }
@@ -2875,9 +2944,16 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
       auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
       const uint32_t* d_nbases = tb->d_neg ? tb->d_neg + offset * G::PW : nullptr;
-      kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, d_nbases, tn, tskip,
-                                                               buckets,
-                                                               xkey, xvalid, xpts);
+      static const int pers = [] {  // workgroups per CU of the persistent G1 form (0: one item per thread)
+        const char* e = getenv("ZKMI_ACC_PERS");
+        return e ? atoi(e) : 0;
+      }();
+      if (G::CW == 8 && pers > 0)
+        k_acc_items_g1p<<<(unsigned)(ctx->num_cus * pers), 256, 0, st>>>(items, &nitems[0], sval, d_bases, d_nbases,
+                                                                        tn, tskip, buckets, xkey, xvalid, xpts);
+      else
+        kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, d_nbases, tn,
+                                                                 tskip, buckets, xkey, xvalid, xpts);
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);
     k_items_combine<GB><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, buckets, xvalid, xpts, &nitems[1]);
@@ -3154,9 +3230,17 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
     src = gathered.data();
   }
   if (job->comm) {  // every rank's status block: one failed rank fails the MSM everywhere
+    const uint32_t sig[3] = {shard_sig0(job), (uint32_t)job->sb, (uint32_t)job->W};
     for (int r = 0; r < nr; r++) {
-      if (src[(size_t)r * job->host_words + job->host_words - job->status_words] != 0) {
+      const uint32_t* stw = src + (size_t)r * job->host_words + job->host_words - job->status_words;
+      if (stw[0] != 0) {
         set_error("msm_sharded: rank %d failed while running its shard", r);
+        msm_job_free(job);
+        return ZKMI_EINVAL;
+      }
+      if (memcmp(stw + 1, sig, sizeof(sig)) != 0) {
+        set_error("msm_sharded: rank %d ran another window plan (its shard's table or window setting changed "
+                  "on that rank only)", r);
         msm_job_free(job);
         return ZKMI_EINVAL;
       }
@@ -3221,45 +3305,76 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
     if (n) lrc = check_size(P, n);
   }
   const std::string lerr = lrc ? std::string(zkmi_last_error()) : std::string();
-  constexpr uint32_t MAGIC = 0x5A4B4D53u;
   const bool plan = !lrc && n;
-  uint32_t hdr[8] = {MAGIC, b ? (uint32_t)b->g2 : 0u, plan ? (uint32_t)P.c : 0u, plan ? (uint32_t)P.W : 0u,
-                     plan ? (uint32_t)P.bb : 0u, plan ? (uint32_t)bg.sb : 0u, lrc ? 1u : 0u, 0u};
-  std::vector<uint32_t> all((size_t)8 * comm->nranks);
-  ZK_TRY(comm_allgather_host(comm, hdr, all.data(), sizeof(hdr)));
-  for (int r = 0; r < comm->nranks; r++) {
-    if (all[(size_t)8 * r + 6] == 0) continue;
-    if (lrc) set_error("%s", lerr.c_str());
-    else set_error("msm_sharded: rank %d failed its local checks", r);
-    return ZKMI_EINVAL;
+  // The plan of this (communicator, shard state) was agreed before: no control
+  // collective on this submit.  Every rank's plan signature still travels in
+  // its status block, so a plan that changed on one rank only fails msm_wait
+  // on every rank.
+  const zkmi_bases::AgreedPlan* hit = nullptr;
+  if (b) {
+    for (const auto& a : b->agreed)
+      if (a.comm_serial == comm->serial && a.n == n && a.window == ctx->msm_window && a.tc == b->tc &&
+          a.tp == b->tp && a.tw == b->tw && a.tbal == b->tbal) {
+        hit = &a;
+        break;
+      }
   }
-  const uint32_t* ref = nullptr;
-  for (int r = 0; r < comm->nranks; r++) {
-    const uint32_t* h = &all[(size_t)8 * r];
-    if (h[0] != MAGIC || h[1] != hdr[1]) {
-      set_error("msm_sharded: rank %d runs a %s MSM (or is out of step)", r, h[1] ? "G2" : "G1");
+  uint32_t agreed[4] = {0, 0, 0, 0};  // c, W, bb, sb of the shards (c = 0: all empty)
+  if (hit) {
+    memcpy(agreed, hit->hdr, sizeof(agreed));
+    if (plan && (agreed[0] != (uint32_t)P.c || agreed[1] != (uint32_t)P.W || agreed[2] != (uint32_t)P.bb ||
+                 agreed[3] != (uint32_t)bg.sb)) {
+      set_error("msm_sharded: this rank's window plan changed since it was agreed");
+      lrc = ZKMI_EINVAL;
+    }
+  } else {
+    constexpr uint32_t MAGIC = 0x5A4B4D53u;
+    uint32_t hdr[8] = {MAGIC, b ? (uint32_t)b->g2 : 0u, plan ? (uint32_t)P.c : 0u, plan ? (uint32_t)P.W : 0u,
+                       plan ? (uint32_t)P.bb : 0u, plan ? (uint32_t)bg.sb : 0u, lrc ? 1u : 0u, 0u};
+    std::vector<uint32_t> all((size_t)8 * comm->nranks);
+    ZK_TRY(comm_allgather_host(comm, hdr, all.data(), sizeof(hdr)));
+    for (int r = 0; r < comm->nranks; r++) {
+      if (all[(size_t)8 * r + 6] == 0) continue;
+      if (lrc) set_error("%s", lerr.c_str());
+      else set_error("msm_sharded: rank %d failed its local checks", r);
       return ZKMI_EINVAL;
     }
-    if (!h[2]) continue;  // empty shard
-    if (!ref) ref = h;
-    else if (memcmp(ref + 2, h + 2, 4 * sizeof(uint32_t)) != 0) {
-      set_error("msm_sharded: window plans differ between ranks (c %u/%u, windows %u/%u): use equal shards "
-                "and the same fixed-base table choice on every rank", ref[2], h[2], ref[3], h[3]);
-      return ZKMI_EINVAL;
+    const uint32_t* ref = nullptr;
+    for (int r = 0; r < comm->nranks; r++) {
+      const uint32_t* h = &all[(size_t)8 * r];
+      if (h[0] != MAGIC || h[1] != hdr[1]) {
+        set_error("msm_sharded: rank %d runs a %s MSM (or is out of step)", r, h[1] ? "G2" : "G1");
+        return ZKMI_EINVAL;
+      }
+      if (!h[2]) continue;  // empty shard
+      if (!ref) ref = h;
+      else if (memcmp(ref + 2, h + 2, 4 * sizeof(uint32_t)) != 0) {
+        set_error("msm_sharded: window plans differ between ranks (c %u/%u, windows %u/%u): use equal shards "
+                  "and the same fixed-base table choice on every rank", ref[2], h[2], ref[3], h[3]);
+        return ZKMI_EINVAL;
+      }
     }
+    if (ref) memcpy(agreed, ref + 2, sizeof(agreed));
+    if (b->agreed.size() >= 16) b->agreed.erase(b->agreed.begin());
+    b->agreed.push_back({comm->serial, n, ctx->msm_window, b->tc, b->tp, b->tw, b->tbal,
+                         {agreed[0], agreed[1], agreed[2], agreed[3]}});
   }
   zkmi_msm_job* job = new_job(ctx, b, P, n);
   job->comm = comm;
-  if (!ref) {  // every shard empty: the sum is infinity, nothing to exchange
+  if (!agreed[0]) {  // every shard empty: the sum is infinity, nothing to exchange
+    if (lrc) {
+      msm_job_free(job);
+      return lrc;  // (the peers exchange nothing either)
+    }
     job->empty = true;
     *out = job;
     return 0;
   }
   job->empty = false;
-  job->c = (int)ref[2];
-  job->W = (int)ref[3];
-  job->bb = (int)ref[4];
-  job->sb = (int)ref[5];
+  job->c = (int)agreed[0];
+  job->W = (int)agreed[1];
+  job->bb = (int)agreed[2];
+  job->sb = (int)agreed[3];
   const int XW = b->g2 ? 64 : 32;
   const size_t words = (size_t)job->W * (job->bb + 1) * job->sb * XW;  // bit sums per rank
   int rc = 0;
@@ -3267,7 +3382,9 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
   // test hook (tests/host/test_sharded_msm.cpp): ZKMI_DEBUG_SHARD_FAIL=<rank>
   // makes that rank fail after the plan agreement, before its exchange
   const char* dbg = getenv("ZKMI_DEBUG_SHARD_FAIL");
-  if (dbg && atoi(dbg) == comm->rank) {
+  if (lrc) {  // local checks failed on a cached plan: join the exchange with a failure status
+    rc = lrc;
+  } else if (dbg && atoi(dbg) == comm->rank) {
     set_error("msm_sharded: injected failure (ZKMI_DEBUG_SHARD_FAIL)");
     rc = ZKMI_EHIP;
   } else if (n) {

@@ -103,6 +103,16 @@ struct zkmi_bases {
   // bucket accumulation gathers -P for a negative digit instead of negating
   // per entry; opt-in (ZKMI_NEG_TABLE=1, measured level), null otherwise.
   uint32_t* d_neg = nullptr;
+  // Window plans agreed with the other ranks of a communicator for this shard
+  // (msm_submit_sharded): the first sharded MSM of a (communicator, n, table
+  // state, window setting) runs the header all-gather, later ones reuse it.
+  struct AgreedPlan {
+    uint64_t comm_serial;
+    size_t n;
+    int window, tc, tp, tw, tbal;
+    uint32_t hdr[4];  // agreed c, W, bb, sb (c = 0: every shard empty)
+  };
+  mutable std::vector<AgreedPlan> agreed;
 };
 
 // Multi-rank communicator (zkmi.h multi-GPU section; comm.hip).
@@ -110,6 +120,7 @@ constexpr int ZKMI_COMM_RCCL = 0;
 constexpr int ZKMI_COMM_HOST = 1;
 struct zkmi_comm {
   zkmi_ctx* ctx = nullptr;
+  uint64_t serial = 0;                  // process-unique (keys zkmi_bases::agreed)
   int nranks = 1, rank = 0, kind = ZKMI_COMM_RCCL;
   void* nccl = nullptr;                 // ncclComm_t (RCCL transport): bit-sum exchanges
   void* nccl_ctl = nullptr;             // split of it for the synchronous plan headers
