@@ -11,6 +11,7 @@ from zelana_amd.gpu import Context  # noqa: E402
 log_n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 lanes = int(os.environ.get("LANES", "3"))
+depth = int(os.environ.get("DEPTH", "0")) or lanes  # MSMs in flight
 n = 1 << log_n
 ctx = Context(0)
 d = ctx.scalars_generate(seed=20, n=n)
@@ -23,7 +24,7 @@ def run(k):
     q, res = [], None
     for _ in range(k):
         q.append(ctx.msm_submit(b, d, n))
-        if len(q) >= lanes:
+        if len(q) >= depth:
             res = ctx.msm_wait(q.pop(0))
     while q:
         res = ctx.msm_wait(q.pop(0))
@@ -36,4 +37,4 @@ t0 = time.perf_counter()
 run(K)
 ctx.sync()
 dt = (time.perf_counter() - t0) / K
-print(f"2^{log_n} lanes={lanes}: {dt*1e3:.4f} ms/step {n/dt/1e6:.1f} Mpt/s", flush=True)
+print(f"2^{log_n} lanes={lanes} depth={depth}: {dt*1e3:.4f} ms/step {n/dt/1e6:.1f} Mpt/s", flush=True)

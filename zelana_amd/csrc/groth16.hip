@@ -233,11 +233,15 @@ __global__ void __launch_bounds__(256) k_to_mont_fr(const uint32_t* __restrict__
 // rows i < m: out[i] = sum_k val_k * z[col_k]  (val canonical, z Montgomery ->
 // canonical product); rows m <= i < m + l of A copy z (inputs appended to A
 // only); the rest of the domain is zero.  (evaluate_constraint, §8a a5)
-// A wave owns 64 consecutive rows.  Rows of at most MATVEC_SHORT terms are
-// summed by their own lane; longer rows (Poseidon/packing rows, 254-term bit
-// recompositions) are summed by the whole wave in turn -- lanes stride over
-// the row's terms, then a 6-level shuffle tree -- so one long row no longer
-// serialises in one lane (config 1's C mat-vec: 262 us one lane per row).
+// Rows of at most MATVEC_SHORT terms are summed one lane per row (blocks
+// below nsb).  The longer rows (Poseidon rounds' inlined linear combinations,
+// 254-term bit recompositions) are listed at upload (upload_r1cs) and summed
+// by lane groups in the blocks from nsb on: g lanes per row, g the power of
+// two that leaves <= 4 terms per lane for the matrix's longest row, then a
+// log2(g)-level shuffle tree; the group's first lane stores the row.  A long
+// row then never serialises in one lane (config 1's C mat-vec took 262 us
+// with one lane per row), and a matrix of many medium rows (config 1's B:
+// 2,040 rows of 9-60 terms) spreads over many waves.
 constexpr uint32_t MATVEC_SHORT = 8;
 __device__ __forceinline__ Fe fe_shfl_xor(const Fe& a, int m) {
   Fe r;
@@ -248,34 +252,34 @@ __device__ __forceinline__ Fe fe_shfl_xor(const Fe& a, int m) {
 __global__ void __launch_bounds__(256) k_matvec(const uint64_t* __restrict__ rowptr, const uint64_t* __restrict__ col,
                                                 const uint32_t* __restrict__ val, const uint32_t* __restrict__ zm,
                                                 const uint32_t* __restrict__ zc, size_t m, size_t l, size_t n,
-                                                int is_a, uint32_t* __restrict__ out) {
-  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // lanes past n join the shuffles
-  const int lane = threadIdx.x & 63;
-  Fe acc = fe_zero();
-  uint64_t k0 = 0, k1 = 0;
-  if (i < m) {
-    k0 = rowptr[i];
-    k1 = rowptr[i + 1];
+                                                int is_a, const uint32_t* __restrict__ lrow, uint32_t nlong, int g,
+                                                uint32_t nsb, uint32_t* __restrict__ out) {
+  if (blockIdx.x < nsb) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fe acc = fe_zero();
+    if (i < m) {
+      const uint64_t k0 = rowptr[i], k1 = rowptr[i + 1];
+      if (k1 - k0 > MATVEC_SHORT) return;  // a long row: the group blocks store it
+      for (uint64_t k = k0; k < k1; k++) acc = add<FrP>(acc, mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8)));
+    } else if (is_a && i < m + l) {
+      acc = ld_fe(zc + (i - m) * 8);
+    }
+    st_fe(out + i * 8, acc);
+    return;
   }
-  const bool longrow = k1 - k0 > MATVEC_SHORT;
-  if (i < m && !longrow) {
-    for (uint64_t k = k0; k < k1; k++) acc = add<FrP>(acc, mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8)));
-  } else if (is_a && i >= m && i < m + l) {
-    acc = ld_fe(zc + (i - m) * 8);
-  }
-  uint64_t pending = __ballot(longrow);  // wave-uniform
-  while (pending) {
-    const int src = __builtin_ctzll(pending);
-    pending &= pending - 1;
-    const uint64_t b0 = __shfl(k0, src, 64), b1 = __shfl(k1, src, 64);
-    Fe part = fe_zero();
-    for (uint64_t k = b0 + lane; k < b1; k += 64)
+  const uint32_t t = (blockIdx.x - nsb) * blockDim.x + threadIdx.x;
+  const uint32_t j = t / (uint32_t)g, gl = t % (uint32_t)g;
+  Fe part = fe_zero();
+  uint32_t row = 0;
+  if (j < nlong) {
+    row = lrow[j];
+    const uint64_t k1 = rowptr[row + 1];
+    for (uint64_t k = rowptr[row] + gl; k < k1; k += (uint32_t)g)
       part = add<FrP>(part, mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8)));
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) part = add<FrP>(part, fe_shfl_xor(part, d));
-    if (lane == src) acc = part;
   }
-  if (i < n) st_fe(out + i * 8, acc);
+  for (int d = g >> 1; d >= 1; d >>= 1) part = add<FrP>(part, fe_shfl_xor(part, d));  // every lane shuffles
+  if (j < nlong && gl == 0) st_fe(out + (size_t)row * 8, part);
 }
 // powers table: tab[x] = c * base^(x * step) for x < cnt (Montgomery), runs of 64
 __global__ void __launch_bounds__(256) k_pow_table(uint32_t* __restrict__ tab, uint32_t cnt, const uint32_t* base_c,
@@ -392,6 +396,10 @@ struct zkmi_r1cs_dev {
   uint64_t* rp[3] = {nullptr, nullptr, nullptr};
   uint64_t* col[3] = {nullptr, nullptr, nullptr};
   uint32_t* val[3] = {nullptr, nullptr, nullptr};
+  // rows longer than MATVEC_SHORT terms (k_matvec's lane-group blocks)
+  uint32_t* lrow[3] = {nullptr, nullptr, nullptr};
+  uint32_t nlong[3] = {0, 0, 0};
+  int glong[3] = {2, 2, 2};  // lanes per long row
   bool owned = false;
   ~zkmi_r1cs_dev() {
     if (!owned) return;
@@ -399,6 +407,7 @@ struct zkmi_r1cs_dev {
       hipFree(rp[t]);
       hipFree(col[t]);
       hipFree(val[t]);
+      if (lrow[t]) hipFree(lrow[t]);
     }
   }
 };
@@ -453,6 +462,34 @@ static int upload_r1cs(zkmi_ctx* ctx, const zkmi_r1cs* cs, DevR1CS* d, bool owne
       ZK_TRY(ctx->ws.get(b2, std::max<uint64_t>(1, nnz) * 8, (void**)&d->col[t]));
       ZK_TRY(ctx->ws.get(b3, std::max<uint64_t>(1, nnz) * 32, (void**)&d->val[t]));
     }
+    // long-row list for k_matvec (synchronous copy: the list is a temporary)
+    std::vector<uint32_t> lr;
+    uint64_t lmax = 0;
+    for (size_t i = 0; i < m; i++) {
+      const uint64_t len = rps[t][i + 1] - rps[t][i];
+      if (len > MATVEC_SHORT) {
+        lr.push_back((uint32_t)i);
+        lmax = std::max(lmax, len);
+      }
+    }
+    d->nlong[t] = (uint32_t)lr.size();
+    d->glong[t] = 2;
+    while (d->glong[t] < 64 && (uint64_t)d->glong[t] * 4 < lmax) d->glong[t] <<= 1;
+    if (!lr.empty()) {
+      if (owned) {
+        if (hipMalloc(&d->lrow[t], lr.size() * 4) != hipSuccess) {
+          (void)hipGetLastError();
+          set_error("r1cs: device allocation failed (matrix %s long rows)", nm[t]);
+          return ZKMI_ENOMEM;
+        }
+      } else {
+        char b4[32];
+        snprintf(b4, 32, "r1cs_long_%s", nm[t]);
+        ZK_TRY(ctx->ws.get(b4, lr.size() * 4, (void**)&d->lrow[t]));
+      }
+      ZK_HIP(hipMemcpyAsync(d->lrow[t], lr.data(), lr.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+      ZK_HIP(hipStreamSynchronize(ctx->stream));
+    }
     ZK_HIP(hipMemcpyAsync(d->rp[t], rps[t], (m + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
     if (nnz) {
       ZK_HIP(hipMemcpyAsync(d->col[t], cols[t], nnz * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -484,9 +521,12 @@ static int witness_map_dev(zkmi_ctx* ctx, const DevR1CS& dr, const uint32_t* d_z
   {
     ScopedKernelTimer tm(ctx, "g16_matvec");
     k_to_mont_fr<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(d_z, nv, zm);
-    k_matvec<<<gn, 256, 0, st>>>(dr.rp[0], dr.col[0], dr.val[0], zm, d_z, m, l, n, 1, a);
-    k_matvec<<<gn, 256, 0, st>>>(dr.rp[1], dr.col[1], dr.val[1], zm, d_z, m, l, n, 0, b);
-    k_matvec<<<gn, 256, 0, st>>>(dr.rp[2], dr.col[2], dr.val[2], zm, d_z, m, l, n, 0, c);
+    uint32_t* outs[3] = {a, b, c};
+    for (int t = 0; t < 3; t++) {
+      const unsigned gl = (unsigned)(((size_t)dr.nlong[t] * dr.glong[t] + 255) / 256);
+      k_matvec<<<gn + gl, 256, 0, st>>>(dr.rp[t], dr.col[t], dr.val[t], zm, d_z, m, l, n, t == 0, dr.lrow[t],
+                                        dr.nlong[t], dr.glong[t], gn, outs[t]);
+    }
     ZK_HIP(hipGetLastError());
   }
   // evaluations -> coefficients (DIF, bit-reversed) -> * n^-1 g^i -> coset

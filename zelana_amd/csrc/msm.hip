@@ -51,6 +51,9 @@ namespace zk {
 #ifndef ZK_TAIL_PRIO
 #define ZK_TAIL_PRIO 3
 #endif
+#ifndef ZK_BR_MINW
+#define ZK_BR_MINW 1
+#endif
 #define ZK_TAIL_WAVE()                                        \
   do {                                                        \
     if (ZK_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(ZK_TAIL_PRIO); \
@@ -1300,7 +1303,10 @@ __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
 // plan's longest-first order.  Launched with fewer waves per SIMD than the
 // kernel's VGPR budget allows, it leaves room for other lanes' sort and
 // bucket-reduction waves to run beside it.
-__global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
+#ifndef ZK_ACCP_MINBLK
+#define ZK_ACCP_MINBLK ZK_ACC0_G1_MINBLK
+#endif
+__global__ void __launch_bounds__(256, ZK_ACCP_MINBLK)
     k_acc_items_g1p(const uint4* __restrict__ items, uint32_t* __restrict__ nitems,
                     const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
                     const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
@@ -1328,7 +1334,7 @@ __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
 // Buckets split into 2..ITEM_SEQ_MAX pieces: one thread sums them (contiguous
 // partial slots) and invalidates them; longer ones stay for k_msm_accN.
 template <class G>
-__global__ void __launch_bounds__(256) k_items_combine(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, 8))) k_items_combine(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
                                                        const uint32_t* __restrict__ pbase,
                                                        uint32_t* __restrict__ buckets, uint32_t* __restrict__ xvalid,
                                                        const uint32_t* __restrict__ xpts,
@@ -1352,7 +1358,7 @@ __global__ void __launch_bounds__(256) k_items_combine(const uint32_t* __restric
 }
 
 template <class G>
-__global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ xkey, const uint32_t* __restrict__ xvalid,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, 8))) k_msm_accN(const uint32_t* __restrict__ xkey, const uint32_t* __restrict__ xvalid,
                                                   const uint32_t* __restrict__ xpts, uint32_t M, uint32_t L,
                                                   uint32_t nchunks, uint32_t* __restrict__ buckets,
                                                   uint32_t* __restrict__ ykey, uint32_t* __restrict__ yvalid,
@@ -1519,8 +1525,9 @@ __device__ __forceinline__ uint32_t insert_bit(uint32_t t, int bit) {
 #ifndef ZK_BR_WPE
 #define ZK_BR_WPE 4
 #endif
+
 template <class G, bool BITS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE))) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
                                                 const uint32_t* __restrict__ bstart, int lb, int hb, int W, int sr,
                                                 int sc, int sb, int segt, uint32_t* __restrict__ out0,
                                                 uint32_t* __restrict__ out1) {
@@ -1633,7 +1640,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
 // jobs (4 folds + 6 levels each), and the bucket reduction runs beside the
 // other lane's accumulation, where wasted VALU issue is what it costs.
 template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br_strip(const uint32_t* __restrict__ buckets,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE))) k_msm_br_strip(const uint32_t* __restrict__ buckets,
                                                       const uint32_t* __restrict__ bstart, int lb, int hb, int W,
                                                       int sr, int sc, int mc, uint32_t* __restrict__ outC,
                                                       uint32_t* __restrict__ outD) {
@@ -1721,7 +1728,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
 //               wave-additions per line for 63 useful lane-additions).
 // Outputs C[w][h] and D[w][l] with one segment per line (sr = sc = 1).
 template <class G, int S>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE)))
     k_br_fold(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ bstart, int lb, int hb, int W,
               uint32_t* __restrict__ part) {
   using F = typename G::F;
@@ -1758,7 +1765,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
 }
 
 template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE)))
     k_br_lines(const uint32_t* __restrict__ part, int lb, int hb, int W, int S, uint32_t nwg_rows,
                uint32_t* __restrict__ outC, uint32_t* __restrict__ outD) {
   using F = typename G::F;
@@ -1835,7 +1842,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
 // 2^18 lanes at 2^19 buckets); only this pass and the bit sums are
 // latency-bound, and they hold one wave per SIMD at most.
 template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE)))
     k_br_strip_p(const uint32_t* __restrict__ part, int lb, int hb, int W, int S, int mc, uint32_t* __restrict__ outC,
                  uint32_t* __restrict__ outD) {
   using F = typename G::F;
