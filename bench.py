@@ -82,8 +82,20 @@ def log(msg):
     print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
+def zk_env():
+    """Every ZK* / ZKMI* variable of this process (recorded in the line's
+    config).  A *DEBUG* one could make the headline skip work (ablation
+    knobs of tools-only builds), so the bench refuses to run with one."""
+    env = {k: v for k, v in sorted(os.environ.items()) if k.startswith(("ZK", "ZKMI"))}
+    bad = [k for k in env if "DEBUG" in k]
+    if bad:
+        sys.exit(f"bench.py: refusing to run with debug variables set: {', '.join(bad)}")
+    return env
+
+
 def main():
     args = parse()
+    env_knobs = zk_env()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -303,6 +315,7 @@ def main():
             "log_n_per_gpu": args.log_n,
             "parallelism": f"point-shard x{world} + RCCL all-gather of partials" if world > 1 else "single GPU",
             "field": "BN254 Fq, 9x29-bit limbs, Montgomery R=2^261",
+            "env": env_knobs,
         },
         "roofline": {
             "bound": "hbm",

@@ -1178,7 +1178,7 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
     v_nxt = v_nn;
     if (p + 2 < end) v_nn = sval[p + 2];
     const uint32_t* w = reinterpret_cast<const uint32_t*>(cr);
-    if (w[G::PW - 1] >> 31) continue;  // base at infinity
+    const bool binf = (w[G::PW - 1] >> 31) != 0;  // base at infinity: mode 3 (no `continue`, see acc_items_g1l)
     Aff<F> P;
     const bool ng = !nbases && (v >> 31);  // sign still to apply (no negated table)
     if constexpr (G::CW == 8) {
@@ -1190,7 +1190,18 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
       P.y = {unpack(w + 16), unpack(w + 24)};
       if (ng) P.y = {fq_cneg(P.y.c0, true), fq_cneg(P.y.c1, true)};
     }
-    acc_step<G>(acc, naff, P);
+    const int mode = binf ? 3 : xyzz_is_inf(acc) ? 0 : (ZK_MMADD && naff) ? 1 : 2;
+    if (mode == 0) {
+      acc = xyzz_from_aff(P);
+      naff = true;
+    } else if (mode == 1) {
+      if constexpr (G::CW == 8) acc = xyzz_mmadd_g1({acc.x, acc.y}, P);
+      else acc = xyzz_mmadd_g2({acc.x, acc.y}, P);
+      naff = false;
+    } else if (mode == 2) {
+      if constexpr (G::CW == 8) acc = xyzz_madd_g1(acc, P);
+      else acc = xyzz_madd_g2(acc, P);
+    }
   }
   if (it.w == NOSLOT) {
     st_acc<G>(buckets + (size_t)it.z * XW, acc);
@@ -1232,7 +1243,7 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
   int phase = 0;  // 0: nothing yet, 1: acc is one affine point, 2: general
   auto step = [&](const uint4 (&r)[4], uint32_t v) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(r);
-    if (w[G1T::PW - 1] >> 31) return;  // base at infinity
+    const int mode = (w[G1T::PW - 1] >> 31) ? 3 : phase;  // 3: base at infinity (see acc_items_g1l)
     const Fe x2 = unpack(w);
     const Fe y0 = unpack(w + 8);
     const Fe yn = bsub(FqP::B2_1, y0);
@@ -1240,14 +1251,14 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
     Fe y2;
 #pragma unroll
     for (int k = 0; k < NL; k++) y2.v[k] = ng ? yn.v[k] : y0.v[k];
-    if (phase == 2) {
+    if (mode == 2) {
       bool inf;
       acc = xyzz_madd_g1f(acc, x2, y2, &inf);
       if (inf) phase = 0;
-    } else if (phase == 1) {
+    } else if (mode == 1) {
       acc = xyzz_mmadd_g1({acc.x, acc.y}, Aff<F>{x2, reduce_q32<FqP>(y2)});
       phase = xyzz_is_inf(acc) ? 0 : 2;
-    } else {
+    } else if (mode == 0) {
       acc = xyzz_from_aff(Aff<F>{x2, reduce_q32<FqP>(y2)});
       phase = 1;
     }
@@ -1303,15 +1314,111 @@ __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
 // plan's longest-first order.  Launched with fewer waves per SIMD than the
 // kernel's VGPR budget allows, it leaves room for other lanes' sort and
 // bucket-reduction waves to run beside it.
-#ifndef ZK_ACCP_MINBLK
-#define ZK_ACCP_MINBLK ZK_ACC0_G1_MINBLK
-#endif
-__global__ void __launch_bounds__(256, ZK_ACCP_MINBLK)
+//
+// Rows come through LDS (global_load_lds_dwordx4, 1 KiB per wave-instruction,
+// lane-linear): the row of entry p + 1 lands in the wave's 4 KiB slot while
+// entry p is added, so no VGPRs hold a row in flight (acc_items_g1f keeps 16).
+// With <= 128 VGPRs three waves per SIMD leave a quarter of the register file
+// to the tail kernels of other lanes (sort, piece sums, bucket reduction), which
+// then run beside the accumulation instead of waiting for it to drain.
+typedef __attribute__((address_space(1))) void zk_gvoid;
+typedef __attribute__((address_space(3))) void zk_lvoid;
+// s_waitcnt encodings (gfx9: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int ZK_WAIT_VM0 = 0x0F70;
+constexpr int ZK_WAIT_LGKM0 = 0xC07F;
+__device__ __forceinline__ void acc_items_g1l(const uint4* __restrict__ items, uint32_t total,
+                                              const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
+                                              const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                                              uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey,
+                                              uint32_t* __restrict__ xvalid, uint32_t* __restrict__ xpts,
+                                              uint32_t i, uint4 (*slot)[64]) {
+  using F = FqOps;
+  constexpr int XW = 32;
+  if (i >= total) return;
+  const int lane = threadIdx.x & 63;
+  const uint4 it = items[i];
+  const uint32_t start = it.x, end = it.y;
+  auto fetch = [&](uint32_t v) {  // row of entry value v -> this lane's slot (async)
+    uint32_t idx = v & 0x7FFFFFFFu;
+    if (tskip) idx += (idx / tn) * tskip;
+    const uint32_t* src = nbases && (v >> 31) ? nbases : bases;
+    const uint4* q = reinterpret_cast<const uint4*>(src + (size_t)idx * G1T::PW);
+#pragma unroll
+    for (int k = 0; k < 4; k++) __builtin_amdgcn_global_load_lds((zk_gvoid*)(q + k), (zk_lvoid*)&slot[k][0], 16, 0, 0);
+  };
+  Xyzz<F> acc = xyzz_inf<F>();
+  int phase = 0;  // 0: nothing yet, 1: acc is one affine point, 2: general
+  const uint32_t last = end - 1;
+  uint32_t v_nxt = sval[start];
+  fetch(v_nxt);
+  uint32_t v_nn = sval[min(start + 1, last)];
+  for (uint32_t p = start; p < end; p++) {
+    const uint32_t v = v_nxt;
+    __builtin_amdgcn_s_waitcnt(ZK_WAIT_VM0);  // this lane's row has landed
+    uint4 cr[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) cr[k] = slot[k][lane];
+    __builtin_amdgcn_s_waitcnt(ZK_WAIT_LGKM0);  // read before the next row overwrites the slot
+    fetch(v_nn);  // unconditional: past the end it re-reads the last entry
+    v_nxt = v_nn;
+    v_nn = sval[min(p + 2, last)];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(cr);
+    // a base at infinity adds nothing: folded into the phase switch (a
+    // `continue` here cost 34 VGPRs: 145 -> 111)
+    const int mode = (w[G1T::PW - 1] >> 31) ? 3 : phase;
+    const Fe x2 = unpack(w);
+    const Fe y0 = unpack(w + 8);
+    const Fe yn = bsub(FqP::B2_1, y0);
+    const bool ng = !nbases && (v >> 31);
+    Fe y2;
+#pragma unroll
+    for (int k = 0; k < NL; k++) y2.v[k] = ng ? yn.v[k] : y0.v[k];
+    if (mode == 2) {
+      int special;
+      acc = xyzz_madd_g1f_nd(acc, x2, y2, &special);
+      if (special == 2) {
+        phase = 0;
+      } else if (special == 1) {  // Q == P (rare): re-read Q and double it
+        uint32_t idx = v & 0x7FFFFFFFu;
+        if (tskip) idx += (idx / tn) * tskip;
+        const uint32_t* src = nbases && (v >> 31) ? nbases : bases;
+        const uint32_t* q = src + (size_t)idx * G1T::PW;
+        const Fe qy0 = unpack(q + 8);
+        const Fe qy = ng ? bsub(FqP::B2_1, qy0) : qy0;
+        acc = xyzz_mdbl(Aff<F>{unpack(q), reduce_q32<FqP>(qy)});
+      }
+    } else if (mode == 1) {
+      acc = xyzz_mmadd_g1({acc.x, acc.y}, Aff<F>{x2, reduce_q32<FqP>(y2)});
+      phase = xyzz_is_inf(acc) ? 0 : 2;
+    } else if (mode == 0) {
+      acc = xyzz_from_aff(Aff<F>{x2, reduce_q32<FqP>(y2)});
+      phase = 1;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(ZK_WAIT_VM0);  // the last (redundant) row lands before the slot is reused
+  if (phase == 0) acc = xyzz_inf<F>();
+  if (it.w == NOSLOT) {
+    st_acc<G1T>(buckets + (size_t)it.z * XW, acc);
+  } else {
+    xkey[it.w] = it.z;
+    xvalid[it.w] = 1;
+    st_acc<G1T>(xpts + (size_t)it.w * XW, acc);
+  }
+}
+// One 768-thread workgroup per CU (grid = CUs): 12 waves = exactly 3 per
+// SIMD whatever the kernel's register count, so the rest of every SIMD's
+// register file (512 - 3 x 120 = 152 VGPRs) and 112 KiB of LDS stay free for
+// the tails of the other lanes.  (768 workgroups of 256 threads did not land 3
+// per CU: at 113 VGPRs the dispatcher packs 4 on some CUs and leaves others
+// empty.)
+constexpr int ACCP_THREADS = 768;
+__global__ void __launch_bounds__(ACCP_THREADS)
     k_acc_items_g1p(const uint4* __restrict__ items, uint32_t* __restrict__ nitems,
                     const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
                     const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
                     uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                     uint32_t* __restrict__ xpts) {
+  __shared__ uint4 rows[ACCP_THREADS / 64][4][64];  // per wave: 4 x 1 KiB, lane-linear
   const uint32_t total = nitems[0];
   const int lane = threadIdx.x & 63;
   for (;;) {
@@ -1319,8 +1426,20 @@ __global__ void __launch_bounds__(256, ZK_ACCP_MINBLK)
     if (lane == 0) base = atomicAdd(&nitems[2], 64u);
     base = (uint32_t)__shfl((int)base, 0, 64);
     if (base >= total) break;
-    acc_items_g1f(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts, base + lane);
+    acc_items_g1l(items, total, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts, base + lane,
+                  rows[threadIdx.x >> 6]);
   }
+}
+// one item per thread, rows through LDS (A/B against k_acc_items_g1)
+__global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
+    k_acc_items_g1l(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
+                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
+                    const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
+                    uint32_t* __restrict__ xpts) {
+  __shared__ uint4 rows[4][4][64];
+  acc_items_g1l(items, nitems[0], sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts,
+                blockIdx.x * blockDim.x + threadIdx.x, rows[threadIdx.x >> 6]);
 }
 __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
     k_acc_items_g2(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
@@ -2644,16 +2763,22 @@ static void scan_excl(hipStream_t st, uint32_t* a, size_t len, uint32_t* bsums, 
   k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
 }
 
-// Timing ablation for development only (tools/ablate_msm.py): ZKMI_DEBUG_SKIP
+// Timing ablation for development only (tools/headline_loop.py): ZKMI_DEBUG_SKIP
 // bit 1 re-uses a lane's previous sort and item plan (valid only when every
 // MSM on the lane has the same scalars), bit 4 skips the bucket reduction
 // (results wrong).  Never set in tests or the bench.
+// Compiled in only by a tools-only build (-DZK_DEBUG_ABLATE, tools/build_ab.sh):
+// the shipped library ignores the variable.
 static int debug_skip() {
+#ifdef ZK_DEBUG_ABLATE
   static const int v = [] {
     const char* e = getenv("ZKMI_DEBUG_SKIP");
     return e ? atoi(e) : 0;
   }();
   return v;
+#else
+  return 0;
+#endif
 }
 
 // Digits + bucket sort on the lane stream: sval (sorted entries) and bstart
@@ -2955,8 +3080,16 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
         const char* e = getenv("ZKMI_ACC_PERS");
         return e ? atoi(e) : 0;
       }();
-      if (G::CW == 8 && pers > 0)
-        k_acc_items_g1p<<<(unsigned)(ctx->num_cus * pers), 256, 0, st>>>(items, &nitems[0], sval, d_bases, d_nbases,
+      static const int lds = [] {
+        const char* e = getenv("ZKMI_ACC_LDS");
+        return e ? atoi(e) : 0;
+      }();
+      if (G::CW == 8 && lds && pers == 0)
+        k_acc_items_g1l<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases,
+                                                                            d_nbases, tn, tskip, buckets, xkey,
+                                                                            xvalid, xpts);
+      else if (G::CW == 8 && pers > 0)
+        k_acc_items_g1p<<<(unsigned)(ctx->num_cus * pers), ACCP_THREADS, 0, st>>>(items, &nitems[0], sval, d_bases, d_nbases,
                                                                         tn, tskip, buckets, xkey, xvalid, xpts);
       else
         kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, d_nbases, tn,
