@@ -181,3 +181,35 @@ def test_msm_2pow20_table_plan_matches_oracle(ctx):
             assert np.array_equal(ctx.msm_wait(j), want)
     finally:
         ctx.set_lanes(2)
+
+
+def test_msm_2pow26_table_plan_matches_oracle(ctx):
+    """Config 5 at its full size: one 2^26 MSM over the
+    c = 22, 12-copy table, as one GPU runs it (bench.py extra.msm_global_2_26,
+    and every rank's shard plan at N = 1), equals the oracle's full 2^26 MSM
+    (ark-ec msm_bigint_wnaf restated, pthreads over windows; ~40 s on 16
+    cores) over the exported bases.  Also the 2-lane pipelined form."""
+    import os
+    import time
+    n = 1 << 26
+    bases = ctx.bases_generate(seed=1026, n=n)
+    info = bases.precompute()
+    assert info[1:] == (22, 12, 1), info
+    d = ctx.scalars_generate(seed=26, n=n)
+    got = ctx.msm(bases, d)
+    ctx.set_lanes(2)
+    try:
+        jobs = [ctx.msm_submit(bases, d, n) for _ in range(2)]
+        piped = [ctx.msm_wait(j) for j in jobs]
+    finally:
+        ctx.set_lanes(2)
+    hs = np.zeros((n, 4), np.uint64)
+    d.download(hs)
+    pts = bases.export()
+    del bases
+    t0 = time.perf_counter()
+    want = O.msm_g1(pts, hs, threads=min(16, os.cpu_count() or 1))
+    print(f"oracle 2^26 MSM: {time.perf_counter() - t0:.1f} s", flush=True)
+    assert np.array_equal(got, want)
+    for p in piped:
+        assert np.array_equal(p, want)

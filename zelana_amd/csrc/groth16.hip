@@ -862,13 +862,10 @@ namespace zk {
 // context stream, then l on lane 1, the B MSMs (the G2 one is the longest
 // chain) on lane 0 of their own, then a and h on lane 1; all z-weighted MSMs
 // fork from one event recorded before the witness map, so they run beside it.
-static size_t small_proof_max() {
-  static const size_t v = [] {
-    const char* e = getenv("ZKMI_SMALL_PROOF_MAX");  // domain size up to which the small schedule applies
-    return e ? (size_t)atoll(e) : (size_t)1 << 16;
-  }();
-  return v;
-}
+// (A hipGraph capture of the whole small proof -- one replay launch instead
+// of ~140 -- measured 3.36 ms against 3.12 ms enqueued as streams: the
+// replayed DAG loses more lane overlap than the launches cost; dropped.)
+constexpr size_t SMALL_PROOF_MAX = (size_t)1 << 16;  // domains up to which the small schedule applies
 static int prove_submit_small(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
                               uint32_t logn, uint32_t* dh, zkmi_msm_job** jobs) {
   const size_t l = dr.l, w = dr.w, nv = l + w, n = pk->n;
@@ -903,156 +900,11 @@ static int prove_submit_small(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& d
   return rc;
 }
 
-// Proof graphs (opt-in, see graphs_enabled).  A small proof is ~140 launches
-// whose enqueueing costs the host ~1 ms: the first synchronous proof of a (key,
-// circuit, z buffer) runs normally and allocates its workspace, the second
-// is captured into a hipGraph (all lanes forked from and joined back into
-// the context stream), and later ones replay it with one launch.  The graph
-// bakes device pointers, so it is dropped when any of them may have moved
-// (graph_gen()); its five MSM jobs keep the pinned buffers their D2H writes,
-// and each replay hands out borrowed copies of them (msm_job_replay).
-// Only zkmi_groth16_prove_resident uses it (one proof in flight at a time).
-struct ProveGraph {
-  const zkmi_pk* pk;
-  const uint32_t* rp0;  // identifies the resident R1CS
-  const uint32_t* dz;
-  size_t m, l, w;
-  uint64_t gen = 0;
-  int uses = 0;  // proofs run for this key (capture on the second)
-  hipGraphExec_t exec = nullptr;
-  zkmi_msm_job* jobs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-};
-static void graph_free(zkmi_ctx* ctx, ProveGraph* g) {
-  if (g->exec) {
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipGraphExecDestroy(g->exec);
-  }
-  for (auto* j : g->jobs) msm_job_release_captured(j);
-  delete g;
-}
-void prove_graphs_free(zkmi_ctx* ctx) {
-  for (void* p : ctx->prove_graphs) graph_free(ctx, (ProveGraph*)p);
-  ctx->prove_graphs.clear();
-}
-// Opt-in (ZKMI_PROVE_GRAPH=1): measured 3.36 ms per configs[0] resident proof
-// replayed against 3.12 ms enqueued as streams (tools/small_prove.py on one
-// box); the replayed DAG loses more lane overlap than the launches cost.
-static bool graphs_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("ZKMI_PROVE_GRAPH");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-static int prove_submit_small(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
-                              uint32_t logn, uint32_t* dh, zkmi_msm_job** jobs);
-// Capture prove_submit_small into g (jobs stay in g).  On failure the context
-// stops using graphs and the caller falls back to a plain submit.
-static int graph_capture(zkmi_ctx* ctx, ProveGraph* g, const DevR1CS& dr, uint32_t logn, uint32_t* dh) {
-  hipStream_t st = ctx->stream;
-  if (hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed) != hipSuccess) {
-    (void)hipGetLastError();
-    return ZKMI_EHIP;
-  }
-  int rc = prove_submit_small(ctx, g->pk, dr, g->dz, logn, dh, g->jobs);
-  // join every lane back into the context stream
-  std::vector<hipEvent_t> joins;
-  for (MsmLane* ln : ctx->lanes) {
-    hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      rc = rc ? rc : ZKMI_EHIP;
-      continue;
-    }
-    joins.push_back(e);
-    if (hipEventRecord(e, ln->st) != hipSuccess || hipStreamWaitEvent(st, e, 0) != hipSuccess) rc = rc ? rc : ZKMI_EHIP;
-  }
-  hipGraph_t graph = nullptr;
-  const hipError_t ee = hipStreamEndCapture(st, &graph);
-  for (hipEvent_t e : joins) (void)hipEventDestroy(e);
-  if (ee != hipSuccess || !graph) rc = rc ? rc : ZKMI_EHIP;
-  if (!rc && hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0) != hipSuccess) {
-    g->exec = nullptr;
-    rc = ZKMI_EHIP;
-  }
-  if (graph) (void)hipGraphDestroy(graph);
-  (void)hipGetLastError();
-  if (rc) {
-    for (auto*& j : g->jobs) {
-      msm_job_release_captured(j);
-      j = nullptr;
-    }
-    set_error("prove graph: capture failed");
-  }
-  return rc;
-}
-// Replay (or capture, then replay) g: the five MSM jobs of this proof in jobs.
-static int graph_launch(zkmi_ctx* ctx, ProveGraph* g, zkmi_msm_job** jobs) {
-  ZK_HIP(hipGraphLaunch(g->exec, ctx->stream));
-  for (int i = 0; i < 5; i++) {
-    jobs[i] = nullptr;
-    if (!g->jobs[i]) continue;
-    hipEvent_t e;
-    ZK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    ZK_HIP(hipEventRecord(e, ctx->stream));
-    jobs[i] = msm_job_replay(g->jobs[i], e);
-  }
-  return 0;
-}
-// prove_submit_small through a graph when possible; returns 1 in *used when it did
-static int prove_submit_graph(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz, uint32_t logn,
-                              uint32_t* dh, zkmi_msm_job** jobs, bool* used) {
-  *used = false;
-  if (ctx->graphs_off || !graphs_enabled() || ctx->timer.enabled) return 0;
-  ProveGraph* g = nullptr;
-  for (size_t i = 0; i < ctx->prove_graphs.size(); i++) {
-    ProveGraph* c = (ProveGraph*)ctx->prove_graphs[i];
-    if (c->pk == pk && c->rp0 == (const uint32_t*)dr.rp[0] && c->dz == dz && c->m == dr.m && c->l == dr.l &&
-        c->w == dr.w) {
-      if (c->gen != graph_gen() && c->exec) {  // stale: drop and count again
-        graph_free(ctx, c);
-        ctx->prove_graphs.erase(ctx->prove_graphs.begin() + i);
-        break;
-      }
-      g = c;
-      break;
-    }
-  }
-  if (!g) {
-    if (ctx->prove_graphs.size() >= 4) {
-      graph_free(ctx, (ProveGraph*)ctx->prove_graphs.front());
-      ctx->prove_graphs.erase(ctx->prove_graphs.begin());
-    }
-    g = new ProveGraph{pk, (const uint32_t*)dr.rp[0], dz, dr.m, dr.l, dr.w};
-    ctx->prove_graphs.push_back(g);
-  }
-  if (++g->uses < 2) return 0;  // first proof of this key: plain (allocates the workspaces)
-  if (!g->exec) {
-    const uint64_t gen0 = graph_gen();
-    if (graph_capture(ctx, g, dr, logn, dh)) {
-      ctx->graphs_off = true;
-      return 0;
-    }
-    if (graph_gen() != gen0) {  // the capture itself allocated: not replayable, retry next time
-      (void)hipGraphExecDestroy(g->exec);
-      g->exec = nullptr;
-      for (auto*& j : g->jobs) {
-        msm_job_release_captured(j);
-        j = nullptr;
-      }
-      return 0;
-    }
-    g->gen = gen0;
-  }
-  ZK_TRY(graph_launch(ctx, g, jobs));
-  *used = true;
-  return 0;
-}
-
 // core: R1CS and full assignment z already resident in HBM.  submit queues
 // everything (the witness map on the context stream, the MSMs on the lanes)
 // and returns; several proofs may be in flight, finished in order by wait.
 int groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
-                         const uint64_t r[4], const uint64_t s[4], zkmi_proof_job** out, bool allow_graph) {
+                         const uint64_t r[4], const uint64_t s[4], zkmi_proof_job** out) {
   *out = nullptr;
   size_t l = dr.l, w = dr.w, nv = l + w;
   uint32_t logn = domain_log(dr.m + l);
@@ -1077,10 +929,8 @@ int groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, co
   zkmi_msm_job** jobs = pj->jobs;
   for (int i = 0; i < 5; i++) jobs[i] = nullptr;
   int rc = 0;
-  if (n <= small_proof_max()) {
-    bool used = false;
-    if (allow_graph) rc = prove_submit_graph(ctx, pk, dr, dz, logn, dh, jobs, &used);
-    if (!rc && !used) rc = prove_submit_small(ctx, pk, dr, dz, logn, dh, jobs);
+  if (n <= SMALL_PROOF_MAX) {
+    rc = prove_submit_small(ctx, pk, dr, dz, logn, dh, jobs);
   } else {
   rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
   if (!rc && pk->d_bidx) {  // a over z[1..V]; b1 / b2 over the compacted B variables
@@ -1133,7 +983,7 @@ int groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, 
                            const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8], uint64_t b_out[16],
                            uint64_t c_out[8]) {
   zkmi_proof_job* pj = nullptr;
-  ZK_TRY(groth16_prove_submit(ctx, pk, dr, dz, r, s, &pj, true));
+  ZK_TRY(groth16_prove_submit(ctx, pk, dr, dz, r, s, &pj));
   return groth16_prove_wait(pj, a_out, b_out, c_out);
 }
 
@@ -1558,12 +1408,8 @@ int zkmi_pk_precompute(zkmi_pk* pk, int factor) {
   const bool compact = pk->d_bidx != nullptr;
   zkmi_bases* qs[5] = {pk->h_query_rev, pk->l_query, pk->a_query, compact ? pk->b_g1_c : pk->b_g1_query,
                        compact ? pk->b_g2_c : pk->b_g2_query};
-  static const size_t min_n = [] {  // experiments: queries below this many bases get no table
-    const char* e = getenv("ZKMI_PK_TABLE_MIN");
-    return e ? (size_t)atoll(e) : (size_t)0;
-  }();
   for (zkmi_bases* b : qs) {
-    if (!b || b->tc || b->n < min_n) continue;
+    if (!b || b->tc) continue;
     int rc = zk::bases_precompute(b, zk::table_window(b->n, b->g2), factor);
     if (rc) return rc;
   }
@@ -1600,7 +1446,6 @@ int zkmi_r1cs_create(zkmi_ctx* ctx, const zkmi_r1cs* cs, zkmi_r1cs_dev** out) {
   return 0;
 }
 void zkmi_r1cs_destroy(zkmi_r1cs_dev* d) {
-  zk::graph_gen_bump();
   delete d;
 }
 int zkmi_groth16_prove_resident(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs_dev* cs, const void* d_z,
@@ -1622,7 +1467,7 @@ int zkmi_groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const zkmi_r1cs_
     set_error("zkmi_groth16_prove_submit: null argument");
     return ZKMI_EINVAL;
   }
-  return groth16_prove_submit(ctx, pk, *cs, (const uint32_t*)d_z, r, s, job, false);
+  return groth16_prove_submit(ctx, pk, *cs, (const uint32_t*)d_z, r, s, job);
 }
 int zkmi_groth16_prove_wait(zkmi_proof_job* job, uint64_t a_out[8], uint64_t b_out[16], uint64_t c_out[8]) {
   if (!job || !a_out || !b_out || !c_out) {

@@ -125,41 +125,16 @@ __device__ __forceinline__ void st_xyzz(uint32_t* p, const Xyzz<typename G::F>& 
   Io<F>::st(p + 3 * G::CW, v.zzz);
 }
 
-#ifndef ZK_MMADD
-#define ZK_MMADD 1
-#endif
-// One bucket-accumulation step acc += P.  The first point of a run is taken
-// as is and the second one added by the affine + affine form (four products
-// fewer than the mixed addition); `naff` tracks "acc is exactly one affine
-// point".  Lanes of a wave run equal trip counts, so the branches are uniform.
-template <class G>
-__device__ __forceinline__ void acc_step(Xyzz<typename G::F>& acc, bool& naff, const Aff<typename G::F>& P) {
-  if (xyzz_is_inf(acc)) {
-    acc = xyzz_from_aff(P);
-    naff = true;
-  } else if (ZK_MMADD && naff) {
-    if constexpr (G::CW == 8) acc = xyzz_mmadd_g1({acc.x, acc.y}, P);
-    else acc = xyzz_mmadd_g2({acc.x, acc.y}, P);
-    naff = false;
-  } else {
-    if constexpr (G::CW == 8) acc = xyzz_madd_g1(acc, P);
-    else acc = xyzz_madd_g2(acc, P);
-  }
-}
 
 // Curve addition of the reductions (piece sums, cascade, bucket reduction).
 // (Split-column products for these 1-2 waves/SIMD kernels -- four independent
 // accumulators per column -- measured no faster: 2^20 lines kernel 217 -> 195
 // us, bit sums 139 -> 143 us; dropped.)
 // The lazy-form additions (ec.h xyzz_add_g1/g2) issue ~15-25% fewer VALU
-// instructions than the generic xyzz_add; ZK_BR_GENERIC=1 keeps the latter.
-#ifndef ZK_BR_GENERIC
-#define ZK_BR_GENERIC 0
-#endif
+// instructions than the generic xyzz_add.
 template <class G>
 __device__ __forceinline__ Xyzz<typename G::F> br_add(const Xyzz<typename G::F>& p, const Xyzz<typename G::F>& q) {
-  if constexpr (ZK_BR_GENERIC) return xyzz_add(p, q);
-  else if constexpr (G::CW == 8) return xyzz_add_g1<typename G::P>(p, q);
+  if constexpr (G::CW == 8) return xyzz_add_g1<typename G::P>(p, q);
   else return xyzz_add_g2(p, q);
 }
 
@@ -502,6 +477,84 @@ __global__ void __launch_bounds__(T) k_rs_p1f_scatter(const uint32_t* __restrict
                                                           okey, oval);
 }
 
+// The same scatter with a small register footprint (256 threads, <= ~64
+// VGPRs): a thread holds only its W ranks; the digits are recomputed from the
+// scalar for the placement pass instead of being held across the block scan.
+// Small enough to run beside the accumulation kernel of another MSM lane
+// (its 3 waves per SIMD leave ~100 VGPRs), where the 1024-thread form needs a
+// whole empty CU.
+template <int C, bool BAL>
+__global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_scatter_lr(const uint32_t* __restrict__ scalars, size_t n,
+                                                                  int Wp, uint32_t B, uint32_t NH, uint32_t lob,
+                                                                  uint32_t CS, uint32_t nc1,
+                                                                  const uint32_t* __restrict__ offs1,
+                                                                  uint32_t* __restrict__ okey,
+                                                                  uint32_t* __restrict__ oval) {
+  ZK_TAIL_WAVE();
+  constexpr int T = RS_THREADS;
+  constexpr int W = msm_windows(C);
+  extern __shared__ uint32_t lds[];
+  uint32_t* hist = lds;
+  uint32_t* lstart = lds + NH;
+  uint32_t* gbase = lds + 2 * NH;
+  uint32_t* tmp = lds + 3 * NH;
+  uint32_t* skey = tmp + T;
+  uint32_t* sv = skey + W * T;
+  for (uint32_t x = threadIdx.x; x < NH; x += T) {
+    gbase[x] = offs1[(size_t)x * nc1 + blockIdx.x];
+    hist[x] = 0;
+  }
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * CS;
+  const uint32_t cnt = (uint32_t)std::min<size_t>(CS, n - base);
+  const uint32_t nsub = (cnt + T - 1) / T;
+  for (uint32_t sub = 0; sub < nsub; sub++) {
+    const uint32_t k = sub * T + threadIdx.x;
+    const size_t i = base + k;
+    uint32_t rk[W];
+    {
+      int32_t d[W];
+      if (k < cnt) scalar_digits<C, BAL>(scalars, i, d);
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        const int32_t v = k < cnt ? d[w] : 0;
+        const uint32_t wq = (uint32_t)(w % Wp);
+        if (v != 0) rk[w] = atomicAdd(&hist[(wq * B + (uint32_t)(v < 0 ? -v : v) - 1) >> lob], 1u);
+      }
+    }
+    __syncthreads();
+    const uint32_t total = rs_block_scan<T>(hist, lstart, NH, tmp);
+    __syncthreads();
+    if (k < cnt) {
+      int32_t d[W];
+      scalar_digits<C, BAL>(scalars, i, d);
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        const int32_t v = d[w];
+        if (v == 0) continue;
+        const uint32_t wq = (uint32_t)(w % Wp), j = (uint32_t)(w / Wp);
+        const uint32_t key = wq * B + (uint32_t)(v < 0 ? -v : v) - 1;
+        const uint32_t lp = lstart[key >> lob] + rk[w];
+        skey[lp] = key;
+        sv[lp] = (uint32_t)(j * n + i) | (v < 0 ? 0x80000000u : 0u);
+      }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < total; q += T) {
+      const uint32_t kk = skey[q], bn = kk >> lob;
+      const uint32_t g = gbase[bn] + (q - lstart[bn]);
+      okey[g] = kk;
+      oval[g] = sv[q];
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < NH; x += T) {
+      gbase[x] += hist[x];
+      hist[x] = 0;
+    }
+    __syncthreads();
+  }
+}
+
 // one workgroup: bin starts and tile starts (tiles of <= C2 entries per bin)
 __global__ void __launch_bounds__(1024) k_rs_tiles(const uint32_t* __restrict__ offs1, uint32_t nc1, uint32_t NH,
                                                    const uint32_t* __restrict__ total, uint32_t C2,
@@ -838,10 +891,6 @@ __device__ __forceinline__ void st_acc(uint32_t* p, Xyzz<typename G::F> v) {
   st_xyzz<G>(p, v);
 }
 
-#ifdef ZK_ACC0_TRACE
-// dev-only (variant builds): per-wave start/end realtime and hardware ids
-__device__ uint64_t zk_acc0_trace[4 * 65536];
-#endif
 template <class G>
 __device__ __forceinline__ void msm_acc0_body(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bstart,
                                                   uint32_t K, uint32_t L, uint32_t nchunks,
@@ -853,25 +902,6 @@ __device__ __forceinline__ void msm_acc0_body(const uint32_t* __restrict__ sval,
   constexpr int XW = 4 * G::CW;
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nchunks) return;
-#ifdef ZK_ACC0_TRACE
-  const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
-  struct TraceEnd {
-    uint32_t t;
-    uint64_t t0;
-    __device__ ~TraceEnd() {
-      if ((t & 63) == 0 && (t >> 6) < 65536) {
-        uint32_t xcc, hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        uint64_t* r = zk_acc0_trace + 4 * (t >> 6);
-        r[0] = t0;
-        r[1] = __builtin_amdgcn_s_memrealtime();
-        r[2] = xcc;
-        r[3] = hw;
-      }
-    }
-  } trace_end{t, tr0};
-#endif
   const uint32_t M = bstart[K];
   uint32_t start = t * L;
   if (t == 0) {
@@ -1131,8 +1161,7 @@ __global__ void __launch_bounds__(256) k_items_scatter(const uint32_t* __restric
 template <class G>
 __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
                                                const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                                               const uint32_t* __restrict__ nbases,
-                                               uint32_t tn, uint32_t tskip, uint32_t* __restrict__ buckets,
+                                                                                              uint32_t tn, uint32_t tskip, uint32_t* __restrict__ buckets,
                                                uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                                                uint32_t* __restrict__ xpts) {
   using F = typename G::F;
@@ -1145,7 +1174,7 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
   auto row = [&](uint32_t v) {
     uint32_t idx = v & 0x7FFFFFFFu;
     if (tskip) idx += (idx / tn) * tskip;
-    const uint32_t* src = nbases && (v >> 31) ? nbases : bases;  // -P rows for a negative digit
+    const uint32_t* src = bases;
     return reinterpret_cast<const uint4*>(src + (size_t)idx * G::PW);
   };
   constexpr bool PF = G::CW == 8;  // G2: see msm_acc0_body
@@ -1180,7 +1209,7 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
     const uint32_t* w = reinterpret_cast<const uint32_t*>(cr);
     const bool binf = (w[G::PW - 1] >> 31) != 0;  // base at infinity: mode 3 (no `continue`, see acc_items_g1l)
     Aff<F> P;
-    const bool ng = !nbases && (v >> 31);  // sign still to apply (no negated table)
+    const bool ng = (v >> 31) != 0;  // negative digit: negate y
     if constexpr (G::CW == 8) {
       P.x = unpack(w);
       P.y = unpack(w + 8);
@@ -1190,7 +1219,7 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
       P.y = {unpack(w + 16), unpack(w + 24)};
       if (ng) P.y = {fq_cneg(P.y.c0, true), fq_cneg(P.y.c1, true)};
     }
-    const int mode = binf ? 3 : xyzz_is_inf(acc) ? 0 : (ZK_MMADD && naff) ? 1 : 2;
+    const int mode = binf ? 3 : xyzz_is_inf(acc) ? 0 : (naff) ? 1 : 2;
     if (mode == 0) {
       acc = xyzz_from_aff(P);
       naff = true;
@@ -1216,15 +1245,12 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
 // taken as is, the second added by the affine + affine form and every later
 // one by xyzz_madd_g1f (subtractions folded into the Montgomery products).  A
 // negative digit's y is the borrow form 2p - y (9 subtractions, no carry
-// pass), or the -P row of the negated table when there is one.  The rare
+// pass).  The rare
 // states (a base at infinity, the empty or one-point accumulator after a
 // cancellation) branch per lane; lanes of a wave have equal trip counts.
-#ifndef ZK_ACC_G1_V1
-#define ZK_ACC_G1_V1 0
-#endif
 __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
                                               const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                                              const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                                              uint32_t tn, uint32_t tskip,
                                               uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey,
                                               uint32_t* __restrict__ xvalid, uint32_t* __restrict__ xpts,
                                               uint32_t i) {
@@ -1236,7 +1262,7 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
   auto row = [&](uint32_t v) {
     uint32_t idx = v & 0x7FFFFFFFu;
     if (tskip) idx += (idx / tn) * tskip;
-    const uint32_t* src = nbases && (v >> 31) ? nbases : bases;  // -P rows for a negative digit
+    const uint32_t* src = bases;
     return reinterpret_cast<const uint4*>(src + (size_t)idx * G1T::PW);
   };
   Xyzz<F> acc = xyzz_inf<F>();
@@ -1247,7 +1273,7 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
     const Fe x2 = unpack(w);
     const Fe y0 = unpack(w + 8);
     const Fe yn = bsub(FqP::B2_1, y0);
-    const bool ng = !nbases && (v >> 31);
+    const bool ng = (v >> 31) != 0;
     Fe y2;
 #pragma unroll
     for (int k = 0; k < NL; k++) y2.v[k] = ng ? yn.v[k] : y0.v[k];
@@ -1302,11 +1328,10 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
 __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
     k_acc_items_g1(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                   const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                   uint32_t tn, uint32_t tskip,
                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                    uint32_t* __restrict__ xpts) {
-  if constexpr (ZK_ACC_G1_V1) acc_items_body<G1T>(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts);
-  else acc_items_g1f(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts,
+  acc_items_g1f(items, nitems, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts,
                      blockIdx.x * blockDim.x + threadIdx.x);
 }
 // Persistent form: a grid of a few workgroups per CU whose waves take 64
@@ -1328,7 +1353,7 @@ constexpr int ZK_WAIT_VM0 = 0x0F70;
 constexpr int ZK_WAIT_LGKM0 = 0xC07F;
 __device__ __forceinline__ void acc_items_g1l(const uint4* __restrict__ items, uint32_t total,
                                               const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                                              const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                                              uint32_t tn, uint32_t tskip,
                                               uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey,
                                               uint32_t* __restrict__ xvalid, uint32_t* __restrict__ xpts,
                                               uint32_t i, uint4 (*slot)[64]) {
@@ -1341,7 +1366,7 @@ __device__ __forceinline__ void acc_items_g1l(const uint4* __restrict__ items, u
   auto fetch = [&](uint32_t v) {  // row of entry value v -> this lane's slot (async)
     uint32_t idx = v & 0x7FFFFFFFu;
     if (tskip) idx += (idx / tn) * tskip;
-    const uint32_t* src = nbases && (v >> 31) ? nbases : bases;
+    const uint32_t* src = bases;
     const uint4* q = reinterpret_cast<const uint4*>(src + (size_t)idx * G1T::PW);
 #pragma unroll
     for (int k = 0; k < 4; k++) __builtin_amdgcn_global_load_lds((zk_gvoid*)(q + k), (zk_lvoid*)&slot[k][0], 16, 0, 0);
@@ -1369,7 +1394,7 @@ __device__ __forceinline__ void acc_items_g1l(const uint4* __restrict__ items, u
     const Fe x2 = unpack(w);
     const Fe y0 = unpack(w + 8);
     const Fe yn = bsub(FqP::B2_1, y0);
-    const bool ng = !nbases && (v >> 31);
+    const bool ng = (v >> 31) != 0;
     Fe y2;
 #pragma unroll
     for (int k = 0; k < NL; k++) y2.v[k] = ng ? yn.v[k] : y0.v[k];
@@ -1381,7 +1406,7 @@ __device__ __forceinline__ void acc_items_g1l(const uint4* __restrict__ items, u
       } else if (special == 1) {  // Q == P (rare): re-read Q and double it
         uint32_t idx = v & 0x7FFFFFFFu;
         if (tskip) idx += (idx / tn) * tskip;
-        const uint32_t* src = nbases && (v >> 31) ? nbases : bases;
+        const uint32_t* src = bases;
         const uint32_t* q = src + (size_t)idx * G1T::PW;
         const Fe qy0 = unpack(q + 8);
         const Fe qy = ng ? bsub(FqP::B2_1, qy0) : qy0;
@@ -1415,7 +1440,7 @@ constexpr int ACCP_THREADS = 768;
 __global__ void __launch_bounds__(ACCP_THREADS)
     k_acc_items_g1p(const uint4* __restrict__ items, uint32_t* __restrict__ nitems,
                     const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                    const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                    uint32_t tn, uint32_t tskip,
                     uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                     uint32_t* __restrict__ xpts) {
   __shared__ uint4 rows[ACCP_THREADS / 64][4][64];  // per wave: 4 x 1 KiB, lane-linear
@@ -1426,7 +1451,7 @@ __global__ void __launch_bounds__(ACCP_THREADS)
     if (lane == 0) base = atomicAdd(&nitems[2], 64u);
     base = (uint32_t)__shfl((int)base, 0, 64);
     if (base >= total) break;
-    acc_items_g1l(items, total, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts, base + lane,
+    acc_items_g1l(items, total, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts, base + lane,
                   rows[threadIdx.x >> 6]);
   }
 }
@@ -1434,20 +1459,20 @@ __global__ void __launch_bounds__(ACCP_THREADS)
 __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
     k_acc_items_g1l(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
                     const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                    const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                    uint32_t tn, uint32_t tskip,
                     uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                     uint32_t* __restrict__ xpts) {
   __shared__ uint4 rows[4][4][64];
-  acc_items_g1l(items, nitems[0], sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts,
+  acc_items_g1l(items, nitems[0], sval, bases, tn, tskip, buckets, xkey, xvalid, xpts,
                 blockIdx.x * blockDim.x + threadIdx.x, rows[threadIdx.x >> 6]);
 }
 __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
     k_acc_items_g2(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                   const uint32_t* __restrict__ nbases, uint32_t tn, uint32_t tskip,
+                   uint32_t tn, uint32_t tskip,
                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
                    uint32_t* __restrict__ xpts) {
-  acc_items_body<G2T>(items, nitems, sval, bases, nbases, tn, tskip, buckets, xkey, xvalid, xpts);
+  acc_items_body<G2T>(items, nitems, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts);
 }
 
 // Buckets split into 2..ITEM_SEQ_MAX pieces: one thread sums them (contiguous
@@ -1831,197 +1856,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_
   if (live && sub == 0) st_xyzz<G>(dst, v);
 }
 
-// Row / column sums in two kernels that keep every issued addition useful
-// (replaces k_msm_br_strip for windows of >= 2^18 buckets):
-//   k_br_fold:  one lane per strip of S buckets of a row or a column, folded
-//               sequentially with the next bucket's load in flight; no tree,
-//               so no lane idles.  Partials: rows (w, h, s) at
-//               ((w << hb) + h) * (2^lb / S) + s, columns (w, s, l) at
-//               nrow + ((w * (2^hb / S) + s) << lb) + l (adjacent lanes read
-//               adjacent columns).
-//   k_br_lines: one workgroup per 256 partials (one line, or 256 / len
-//               lines), a pairwise tree through LDS whose additions are
-//               packed into the lowest lanes at every level, so a level of
-//               k additions costs ceil(k / 64) wave-additions instead of one
-//               per line (k_msm_br_strip's 6-level in-wave tree issued 6
-//               wave-additions per line for 63 useful lane-additions).
-// Outputs C[w][h] and D[w][l] with one segment per line (sr = sc = 1).
-template <class G, int S>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE)))
-    k_br_fold(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ bstart, int lb, int hb, int W,
-              uint32_t* __restrict__ part) {
-  using F = typename G::F;
-  constexpr int XW = 4 * G::CW;
-  const int bb = lb + hb;
-  const uint32_t per_w = (1u << bb) / S;  // strips per window, per direction
-  const uint32_t nrow = (uint32_t)W * per_w;
-  const uint32_t task = blockIdx.x * 256 + threadIdx.x;
-  if (task >= 2 * nrow) return;
-  uint32_t b0, stride;
-  if (task < nrow) {
-    const uint32_t w = task / per_w, r = task % per_w;
-    const uint32_t h = r / ((1u << lb) / S), s = r % ((1u << lb) / S);
-    b0 = (w << bb) + (h << lb) + s * S;
-    stride = 1;
-  } else {
-    const uint32_t c = task - nrow, w = c / per_w, r = c % per_w;
-    const uint32_t s = r >> lb, l = r & ((1u << lb) - 1);
-    b0 = (w << bb) + ((s * S) << lb) + l;
-    stride = 1u << lb;
-  }
-  Xyzz<F> v = xyzz_inf<F>();
-  Xyzz<F> q = bstart[b0 + 1] > bstart[b0] ? ld_xyzz<G>(buckets + (size_t)b0 * XW) : xyzz_inf<F>();
-  for (int k = 0; k < S; k++) {
-    Xyzz<F> qn = xyzz_inf<F>();
-    if (k + 1 < S) {
-      const uint32_t b = b0 + (uint32_t)(k + 1) * stride;
-      if (bstart[b + 1] > bstart[b]) qn = ld_xyzz<G>(buckets + (size_t)b * XW);
-    }
-    v = br_add<G>(v, q);
-    q = qn;
-  }
-  st_xyzz<G>(part + (size_t)task * XW, v);
-}
-
-template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE)))
-    k_br_lines(const uint32_t* __restrict__ part, int lb, int hb, int W, int S, uint32_t nwg_rows,
-               uint32_t* __restrict__ outC, uint32_t* __restrict__ outD) {
-  using F = typename G::F;
-  constexpr int XW = 4 * G::CW;
-  extern __shared__ uint32_t sh[];  // 256 packed XYZZ
-  const int bb = lb + hb;
-  const bool rows = blockIdx.x < nwg_rows;
-  const uint32_t len = rows ? (1u << lb) / S : (1u << hb) / S;  // partials per line
-  const uint32_t lenp = len < 256 ? len : 256;                  // per line in the tree
-  const uint32_t m = 256 / lenp;                                // lines per workgroup
-  const uint32_t f = len / lenp;                                // partials folded per lane
-  const uint32_t g = rows ? blockIdx.x : blockIdx.x - nwg_rows;
-  const uint32_t t = threadIdx.x;
-  // load: rows read contiguous partials; columns put adjacent lines on
-  // adjacent lanes (adjacent addresses)
-  uint32_t i, p;
-  if (rows) {
-    i = t / lenp;
-    p = t % lenp;
-  } else {
-    i = t % m;
-    p = t / m;
-  }
-  const uint32_t line = g * m + i;  // (w << hb) + h, or (w << lb) + l
-  uint32_t levels = 0;
-  while ((1u << levels) < lenp) levels++;
-  // one curve-addition call site: f fold steps, then the tree levels
-  Xyzz<F> v = xyzz_inf<F>();
-  for (uint32_t step = 0; step < f + levels; step++) {
-    Xyzz<F> a, b;
-    bool act = true;
-    uint32_t* dst = nullptr;
-    if (step < f) {
-      const uint32_t s = step * lenp + p;
-      size_t idx;
-      if (rows) {
-        idx = (size_t)line * len + s;
-      } else {
-        const uint32_t w = line >> lb, l = line & ((1u << lb) - 1);
-        idx = ((size_t)W << bb) / S + (((size_t)w * len + s) << lb) + l;
-      }
-      a = v;
-      b = ld_xyzz<G>(part + idx * XW);
-    } else {
-      const uint32_t half = lenp >> (step - f + 1);
-      act = t < m * half;
-      if (act) {
-        dst = sh + (size_t)((t / half) * lenp + t % half) * XW;
-        a = ld_xyzz<G>(dst);
-        b = ld_xyzz<G>(dst + (size_t)half * XW);
-      }
-    }
-    if (act) {
-      const Xyzz<F> r = br_add<G>(a, b);
-      if (step < f) v = r;
-      else st_xyzz<G>(dst, r);
-    }
-    if (step + 1 == f) st_xyzz<G>(sh + (size_t)(i * lenp + p) * XW, v);
-    if (step + 1 >= f) __syncthreads();
-  }
-  if (t < m) {
-    const uint32_t ln = g * m + t;
-    const uint32_t* src = sh + (size_t)(t * lenp) * XW;
-    uint32_t* dst = (rows ? outC : outD) + (size_t)ln * XW;
-    for (int k = 0; k < XW; k++) dst[k] = src[k];
-  }
-}
-
-// Mode 3, second pass: the k_br_fold partials of a line summed by one wave
-// (rows: 64 lanes, contiguous strips of 2^lb / S / 64 partials) or by mc lanes
-// (columns: 64 / mc columns per wave), then the in-wave tree of
-// k_msm_br_strip.  Outputs C[w][h], D[w][l] (sr = sc = 1).  k_br_fold runs
-// every addition of the first pass at full occupancy (one lane per S buckets,
-// 2^18 lanes at 2^19 buckets); only this pass and the bit sums are
-// latency-bound, and they hold one wave per SIMD at most.
-template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE)))
-    k_br_strip_p(const uint32_t* __restrict__ part, int lb, int hb, int W, int S, int mc, uint32_t* __restrict__ outC,
-                 uint32_t* __restrict__ outD) {
-  using F = typename G::F;
-  constexpr int XW = 4 * G::CW;
-  __shared__ Xyzz<F> sh[4][32];
-  const int bb = lb + hb;
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t job = blockIdx.x * 4 + wave;
-  const uint32_t nrow = (uint32_t)W << hb, ncol = (uint32_t)W << lb;
-  const uint32_t Lr = (1u << lb) / S, Lc = (1u << hb) / S;  // partials per row / column line
-  const uint32_t cpw = 64u / (uint32_t)mc;
-  const bool row_wave = job < nrow;
-  const uint32_t m = row_wave ? 64u : (uint32_t)mc;
-  const uint32_t sub = lane & (m - 1), lslot = (lane / m) * (m / 2);
-  bool live = false;
-  size_t base = 0, stride = 1;
-  uint32_t len = 0;
-  uint32_t* dst = nullptr;
-  if (row_wave) {
-    live = true;
-    len = Lr;
-    base = (size_t)job * Lr;
-    dst = outC + (size_t)job * XW;
-  } else {
-    const uint32_t jj = (job - nrow) * cpw + lane / m;  // (w << lb) + l
-    if (jj < ncol) {
-      const uint32_t w = jj >> lb, l = jj & ((1u << lb) - 1);
-      live = true;
-      len = Lc;
-      base = ((size_t)W << bb) / S + (((size_t)w * Lc) << lb) + l;
-      stride = (size_t)1 << lb;
-      dst = outD + (size_t)jj * XW;
-    }
-  }
-  const uint32_t L = (len + m - 1) / m;
-  const uint32_t Lmax = ((Lr + 63) / 64) > ((Lc + mc - 1) / mc) ? (Lr + 63) / 64 : (Lc + mc - 1) / mc;
-  Xyzz<F> v = xyzz_inf<F>();
-  for (uint32_t step = 0; step < Lmax + 6; step++) {
-    Xyzz<F> q;
-    bool act = false;
-    if (step < Lmax) {
-      const uint32_t t = sub * L + step;
-      if (live && step < L && t < len) {
-        q = ld_xyzz<G>(part + (base + (size_t)t * stride) * XW);
-        act = !xyzz_is_inf(q);
-      }
-    } else {
-      const uint32_t sz = 32u >> (step - Lmax);
-      if (sz < m && sub >= sz && sub < 2 * sz) sh[wave][lslot + sub - sz] = v;
-      __syncthreads();
-      if (sz < m && sub < sz) {
-        q = sh[wave][lslot + sub];
-        act = !xyzz_is_inf(q);
-      }
-    }
-    if (act) v = xyzz_is_inf(v) ? q : br_add<G>(v, q);
-    if (step >= Lmax) __syncthreads();
-  }
-  if (live && sub == 0) st_xyzz<G>(dst, v);
-}
+// (Tried: row / column sums as per-strip folds + an LDS-packed line tree
+// (issues ~35% fewer wave-additions, 0.38 vs 0.45 ms isolated), and the folds
+// + a second in-wave strip pass: level or slower in the pipelined MSM and 2-7%
+// slower in the proofs; dropped.)
 
 // ------------------------------------------------------------ base upload
 // canonical affine (x||y, all-zero = infinity) -> internal Montgomery packed,
@@ -2475,29 +2313,8 @@ int bases_upload(zkmi_ctx* ctx, int g2, const uint64_t* host_affine, size_t n, z
 
 // neg[r] = (x, 2p - y) for every table row r (both Fq2 components for G2) --
 // exactly the y that fq_cneg produces -- infinity rows copied as they are
-template <class G>
-__global__ void __launch_bounds__(256) k_bases_negate(const uint32_t* __restrict__ in, size_t rows,
-                                                      uint32_t* __restrict__ out) {
-  const size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (r >= rows) return;
-  const uint32_t* p = in + r * G::PW;
-  uint32_t* q = out + r * G::PW;
-  uint32_t w[G::PW];
-#pragma unroll
-  for (int k = 0; k < G::PW; k++) w[k] = p[k];
-  if (!(w[G::PW - 1] >> 31)) {
-#pragma unroll
-    for (int c = G::PW / 2; c < G::PW; c += 8) {  // the y components
-      const Fe y = fq_cneg(unpack(w + c), true);
-      pack(w + c, y);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < G::PW; k++) q[k] = w[k];
-}
 
 int bases_precompute(zkmi_bases* b, int c, int factor) {
-  graph_gen_bump();
   if (c < 4 || c > 22) {
     set_error("bases_precompute: window %d outside [4, 22]", c);
     return ZKMI_EINVAL;
@@ -2531,12 +2348,7 @@ int bases_precompute(zkmi_bases* b, int c, int factor) {
   if (e == hipSuccess && b->n) e = hipMemcpyAsync(d_tab, b->d_pts, b->n * pw * 4, hipMemcpyDeviceToDevice, st);
   // full tables (one window per copy) use the balanced widths (WinLayout):
   // no short top window piling a copy's entries onto a few buckets.
-  // ZKMI_TABLE_BAL=0 keeps the uniform layout (A/B only).
-  static const bool bal_env = [] {
-    const char* e = getenv("ZKMI_TABLE_BAL");
-    return !e || atoi(e) != 0;
-  }();
-  const bool bal = bal_env && Wp == 1 && c >= 4;
+  const bool bal = Wp == 1 && c >= 4;
   const int wide = bal ? std::max(0, 254 - W * (c - 1)) : p;
   if (e == hipSuccess && b->n && p > 1) {
     unsigned grid = (unsigned)((b->n + 255) / 256);
@@ -2558,32 +2370,9 @@ int bases_precompute(zkmi_bases* b, int c, int factor) {
   b->tp = p;
   b->tw = Wp;
   b->tbal = bal ? 1 : 0;
-  // negated copy for the one-lane-per-bucket path (2^(c-1) >= ITEMS_MIN_K),
-  // only while HBM stays comfortably free (MSM workspaces come later)
-  // Opt-in (ZKMI_NEG_TABLE=1): the gathers then spread over twice the table,
-  // which cancels the ~60 instructions per entry it saves (tools/neg_ab2.sh:
-  // 2^20 3-lane 830-836 Mpt/s either way, 2^26 984 with vs 997 without), and
-  // it doubles the table's HBM.
-  static const bool use_neg = [] {
-    const char* e = getenv("ZKMI_NEG_TABLE");
-    return e && atoi(e) != 0;
-  }();
-  if (use_neg && (1u << (c - 1)) >= ITEMS_MIN_K && b->n) {
-    size_t fr = 0, tot = 0;
-    const size_t bytes = row * p;
-    if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 2 * bytes + ((size_t)16 << 30)) {
-      uint32_t* d_neg = nullptr;
-      if (hipMalloc(&d_neg, bytes) == hipSuccess) {
-        const size_t rows = b->n * (size_t)p;
-        const unsigned grid = (unsigned)((rows + 255) / 256);
-        if (b->g2) k_bases_negate<G2T><<<grid, 256, 0, st>>>(d_tab, rows, d_neg);
-        else k_bases_negate<G1T><<<grid, 256, 0, st>>>(d_tab, rows, d_neg);
-        if (hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess) b->d_neg = d_neg;
-        else hipFree(d_neg);
-      }
-      (void)hipGetLastError();
-    }
-  }
+  // (A negated copy of the table -- gather -P for a negative digit instead of
+  // negating y per entry, ~60 instructions -- measured level at 2^20 and 1.3%
+  // slower at 2^26 while doubling the table's HBM; dropped.)
   return 0;
 }
 
@@ -2591,11 +2380,6 @@ int bases_precompute(zkmi_bases* b, int c, int factor) {
 // buckets; bucket reduction costs ~2.5 additions per bucket.  From 2^18
 // buckets on, the accumulation runs one lane per bucket (k_acc_items).
 int table_window(size_t N, int g2) {
-  static const int env_c = [] {
-    const char* e = getenv("ZKMI_TABLE_C");  // experiments: pin the table window
-    return e ? atoi(e) : 0;
-  }();
-  if (env_c >= 4 && env_c <= 22) return env_c;
   // (G2: c = 17 below 2^21 points is faster for a lone MSM, 2^19: 4.45 ->
   // 3.50 ms, but in a prove it splits B1 / B2's shared sort: zelana_batch 66
   // -> 61 proofs/s.  Same window for both groups.)
@@ -2658,7 +2442,10 @@ static void launch_p1_fused(hipStream_t st, const uint32_t* sc, size_t n, int Wp
     return e ? atoi(e) : 1024;
   }();
   constexpr int W = msm_windows(C);
-  if (scatter && env_t1 == 1024 && rs_scatter_lds(NH, 1024 * W, 1024) <= 160 * 1024)
+  if (scatter && env_t1 == 2)  // low-register 256-thread form (co-resides with an accumulation)
+    k_rs_p1f_scatter_lr<C, BAL><<<nf, RS_THREADS, rs_scatter_lds(NH, RS_THREADS * W), st>>>(
+        sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval);
+  else if (scatter && env_t1 == 1024 && rs_scatter_lds(NH, 1024 * W, 1024) <= 160 * 1024)
     k_rs_p1f_scatter<C, 1024, BAL><<<nf, 1024, rs_scatter_lds(NH, 1024 * W, 1024), st>>>(sc, n, Wp, B, NH, lob, CS, nf,
                                                                                     cnt1, okey, oval);
   else if (scatter)
@@ -2702,7 +2489,6 @@ struct zkmi_msm_job {
   zkmi_comm* comm = nullptr;    // sharded MSM: bit sums of every rank are summed
   size_t status_words = 0;      // sharded: status block after the bit sums (per rank)
   bool exchanged = false;       // sharded over RCCL: the data all-gather is queued
-  bool borrowed = false;        // graph replay: `host` belongs to the captured job
 };
 
 namespace zk {
@@ -2900,16 +2686,10 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
 // Bucket-reduction geometry of a plan.
 //   mode 1 (windows with rows / columns of >= 2^9 buckets, i.e. the >= 2^18
 //     bucket tables): k_msm_br_strip waves of 8 (G1) / 16 (G2) buckets per
-//     lane and a 6-level in-wave tree.
-//   mode 2 (ZKMI_BR_MODE=2, same windows): k_br_fold (S buckets per lane) +
-//     k_br_lines, one C / D segment per line (sr = sc = 1).  Issues ~35% fewer
-//     wave-additions and is 15% faster isolated (2^20 table: 0.38 vs 0.45 ms),
-//     but in the pipelined bench it was level for the 2^20 MSM (755-765 both)
-//     and lost 2-7% in the proofs (L2 27.7 -> 27.0/s, zelana_batch end to end
-//     47.7 -> 44.4/s), so it stays opt-in.  Every level of either form runs
-//     at 1-2 waves per SIMD, where one full XYZZ addition takes ~15-20 us (vs
-//     ~5.5 us of issue at 4+ waves): the ~19 dependent additions from 2^19
-//     buckets to the bit sums set the isolated time.
+//     lane and a 6-level in-wave tree.  Every level runs at 1-2 waves per
+//     SIMD, where one full XYZZ addition takes ~15-20 us (vs ~5.5 us of issue
+//     at 4+ waves): the ~19 dependent additions from 2^19 buckets to the bit
+//     sums set the isolated time.
 //   mode 0 (smaller windows): <= 256-bucket strided wave jobs (k_msm_br).
 // Bit sums: sb segments of segt terms each (the longest bit job sums
 // max(2^hb * sr, 2^(lb-1) * sc) terms); the host adds the segments.  Shorter
@@ -2917,57 +2697,24 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
 // waves on an otherwise idle chip) for a few more host additions.
 struct BrGeom {
   int mode;
-  int S;  // mode 2: buckets per lane in k_br_fold
   int sr, sc, sb, segt;
   int mc = 64;  // mode 1: lanes per column segment (k_msm_br_strip)
 };
 static BrGeom br_geom(const MsmPlan& P, bool g2) {
-  static const int env_mode = [] {
-    const char* e = getenv("ZKMI_BR_MODE");
-    return e ? atoi(e) : 1;
-  }();
-  static const int strip_fold = [] {  // mode 1: buckets folded per lane before the tree
-    const char* e = getenv("ZKMI_BR_STRIP");
-    return e ? atoi(e) : 8;  // 16 (+ two 512-bucket columns per wave) measured slower: 2^20 1 lane 0.38 -> 0.46 ms
-  }();
-  static const int strip_fold2 = [] {  // mode 1, G2 (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
-    const char* e = getenv("ZKMI_BR_STRIP_G2");
-    return e ? atoi(e) : 16;
-  }();
-  // mode 2 defaults, 2^20 table MSM with 3 lanes (tools/br_ab2.sh, interleaved
-  // repeats in tools/perf_table.py): mode 1 1.374 ms/MSM, S = 8 / 128-term
-  // segments 1.312 ms, S = 4 1.342 ms (not reproduced by bench.py, above).
-  static const int env_fold = [] {  // mode 2: buckets per lane (4 or 8)
-    const char* e = getenv("ZKMI_BR_FOLD");
-    return e ? atoi(e) : 0;
-  }();
-  static const int env_seg = [] {  // mode 2: terms per bit-sum segment (64, 128, 256)
-    const char* e = getenv("ZKMI_BR_SEG");
-    return e ? atoi(e) : 0;
-  }();
+  // buckets folded per lane before the tree: G1 8 (16 with two 512-bucket
+  // columns per wave measured slower: 2^20 one lane 0.38 -> 0.46 ms); G2 16
+  // (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
+  const int fold = g2 ? 16 : 8;
   BrGeom g;
-  g.mode = P.hb >= 9 ? (env_mode == 2 || env_mode == 3 ? env_mode : 1) : 0;
-  g.S = env_fold == 4 ? 4 : 8;
-  g.segt = env_seg == 64 || env_seg == 128 ? env_seg : 256;
-  if (g.mode == 2) {
-    g.sr = g.sc = 1;
-    g.segt = env_seg == 64 || env_seg == 256 ? env_seg : 128;
-  } else if (g.mode == 3) {
-    g.sr = g.sc = 1;
-    g.S = env_fold == 8 ? 8 : 4;
-    const int lenc = (1 << P.hb) / g.S;  // column partials per line
-    g.mc = 64;
-    while (g.mc > 1 && lenc / g.mc < 4) g.mc >>= 1;
-  } else {
-    const int fold = g2 ? strip_fold2 : strip_fold;
-    const int segb = g.mode == 1 ? 64 * fold : 256;  // buckets per wave job
-    g.sr = (1 << P.lb) > segb ? (1 << P.lb) / segb : 1;
-    g.sc = (1 << P.hb) > segb ? (1 << P.hb) / segb : 1;
-    // lanes per column segment: as many as keep `fold` buckets per lane
-    const int lenc = (1 << P.hb) / g.sc;
-    g.mc = 64;
-    while (g.mc > 1 && lenc / g.mc < fold) g.mc >>= 1;
-  }
+  g.mode = P.hb >= 9 ? 1 : 0;
+  g.segt = 256;
+  const int segb = g.mode == 1 ? 64 * fold : 256;  // buckets per wave job
+  g.sr = (1 << P.lb) > segb ? (1 << P.lb) / segb : 1;
+  g.sc = (1 << P.hb) > segb ? (1 << P.hb) / segb : 1;
+  // lanes per column segment: as many as keep `fold` buckets per lane
+  const int lenc = (1 << P.hb) / g.sc;
+  g.mc = 64;
+  while (g.mc > 1 && lenc / g.mc < fold) g.mc >>= 1;
   const uint32_t maxterms = std::max((1u << P.hb) * g.sr, (1u << (P.lb - 1)) * g.sc);
   g.sb = (int)((maxterms + g.segt - 1) / g.segt);
   return g;
@@ -3020,10 +2767,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
                          size_t n, const uint32_t* sval, const uint32_t* bstart, zkmi_msm_job* job) {
   constexpr int XW = 4 * G::CW;
   using GS = std::conditional_t<G::CW == 8, G1Tn, G>;  // the small-MSM kernels' trait
-#ifndef ZK_BR_N
-#define ZK_BR_N 0  // 1: the large-MSM bucket reductions with GS too (A/B)
-#endif
-  using GB = std::conditional_t<ZK_BR_N != 0, GS, G>;
+  using GB = G;  // (the compiler-scheduled GS products lost here: 3-lane 2^20 862 -> 846-853 Mpt/s)
   hipStream_t st = lane->st;
   Workspace& ws = lane->ws;
   const uint32_t* d_bases = tb->d_pts + offset * G::PW;
@@ -3075,7 +2819,6 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     {
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
       auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
-      const uint32_t* d_nbases = tb->d_neg ? tb->d_neg + offset * G::PW : nullptr;
       static const int pers = [] {  // workgroups per CU of the persistent G1 form (0: one item per thread)
         const char* e = getenv("ZKMI_ACC_PERS");
         return e ? atoi(e) : 0;
@@ -3086,13 +2829,13 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       }();
       if (G::CW == 8 && lds && pers == 0)
         k_acc_items_g1l<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases,
-                                                                            d_nbases, tn, tskip, buckets, xkey,
+                                                                            tn, tskip, buckets, xkey,
                                                                             xvalid, xpts);
       else if (G::CW == 8 && pers > 0)
-        k_acc_items_g1p<<<(unsigned)(ctx->num_cus * pers), ACCP_THREADS, 0, st>>>(items, &nitems[0], sval, d_bases, d_nbases,
+        k_acc_items_g1p<<<(unsigned)(ctx->num_cus * pers), ACCP_THREADS, 0, st>>>(items, &nitems[0], sval, d_bases,
                                                                         tn, tskip, buckets, xkey, xvalid, xpts);
       else
-        kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, d_nbases, tn,
+        kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, tn,
                                                                  tskip, buckets, xkey, xvalid, xpts);
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);
@@ -3102,12 +2845,8 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     // level 0: fixed-size chunks of the sorted list (sized from the upper bound
     // W*n so no host round-trip is needed; chunks past M exit at once).
     // Threads per CU: measured best at ~1024 for G1 (over-subscribing the
-    // resident waves evens out per-thread run lengths); ZKMI_ACC_TPC overrides.
-    static const size_t tpc_env = [] {
-      const char* e = getenv("ZKMI_ACC_TPC");
-      return e ? (size_t)atol(e) : (size_t)0;
-    }();
-    const size_t tpc = tpc_env ? tpc_env : 1024;
+    // resident waves evens out per-thread run lengths).
+    const size_t tpc = 1024;
     const size_t acc_threads = (size_t)ctx->num_cus * tpc;
     uint32_t L = (uint32_t)std::max<size_t>(4, (Mmax + acc_threads - 1) / acc_threads);
     uint32_t nch = (uint32_t)((Mmax + L - 1) / L);
@@ -3174,27 +2913,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   if (!(debug_skip() & 4)) {
     ScopedKernelTimer tm(ctx, "msm_bucket_reduce", brs);
     uint32_t jobs2 = (uint32_t)W * (bb + 1) * sb;
-    if (bg.mode == 2) {
-      const uint32_t nstrips = (uint32_t)W * ((1u << bb) / bg.S);  // per direction
-      uint32_t* part;
-      ZK_TRY(ws.get("msm_brpart", (size_t)2 * nstrips * XW * 4, (void**)&part));
-      const unsigned g1 = (2 * nstrips + 255) / 256;
-      if (bg.S == 8) k_br_fold<G, 8><<<g1, 256, 0, brs>>>(buckets, bstart, lb, hb, W, part);
-      else k_br_fold<G, 4><<<g1, 256, 0, brs>>>(buckets, bstart, lb, hb, W, part);
-      auto wgs = [](uint32_t lines, uint32_t len) { return len >= 256 ? lines : lines / (256 / len); };
-      const uint32_t nwr = wgs((uint32_t)W << hb, (1u << lb) / bg.S), nwc = wgs((uint32_t)W << lb, (1u << hb) / bg.S);
-      k_br_lines<G><<<nwr + nwc, 256, 256 * XW * 4, brs>>>(part, lb, hb, W, bg.S, nwr, Cb, Db);
-    } else if (bg.mode == 3) {
-      const uint32_t nstrips = (uint32_t)W * ((1u << bb) / bg.S);  // per direction
-      uint32_t* part;
-      ZK_TRY(ws.get("msm_brpart", (size_t)2 * nstrips * XW * 4, (void**)&part));
-      const unsigned g1 = (2 * nstrips + 255) / 256;
-      if (bg.S == 8) k_br_fold<G, 8><<<g1, 256, 0, brs>>>(buckets, bstart, lb, hb, W, part);
-      else k_br_fold<G, 4><<<g1, 256, 0, brs>>>(buckets, bstart, lb, hb, W, part);
-      const uint32_t nrow = (uint32_t)W << hb, ncol = (uint32_t)W << lb, cpw = 64u / (uint32_t)bg.mc;
-      const uint32_t jobs1 = nrow + (ncol + cpw - 1) / cpw;
-      k_br_strip_p<G><<<(jobs1 + 3) / 4, 256, 0, brs>>>(part, lb, hb, W, bg.S, bg.mc, Cb, Db);
-    } else if (bg.mode == 1) {  // one wave per row segment, 64 / mc column segments per wave
+    if (bg.mode == 1) {  // one wave per row segment, 64 / mc column segments per wave
       const uint32_t nrow = (uint32_t)W * ((1u << hb) * sr), ncol = (uint32_t)W * ((1u << lb) * sc);
       const uint32_t cpw = 64u / (uint32_t)bg.mc;
       const uint32_t jobs1 = nrow + (ncol + cpw - 1) / cpw;
@@ -3230,12 +2949,6 @@ static int check_size(const MsmPlan& P, size_t n) {
   return 0;
 }
 
-#ifdef ZK_ACC0_TRACE
-extern "C" int zkmi_debug_acc0_trace(uint64_t* out, size_t nwaves) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zk_acc0_trace), nwaves * 32, 0, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-  return 0;
-}
-#endif
 static int check_range(const zkmi_bases* b, size_t offset, size_t n) {
   if (!b || offset > b->n || n > b->n - offset) {
     set_error("msm: range [%zu, %zu) outside base set of %zu", offset, offset + n, b ? b->n : 0);
@@ -3306,21 +3019,8 @@ void msm_job_free(zkmi_msm_job* job) {
     }
   }
   if (job->done) hipEventDestroy(job->done);
-  if (job->host && !job->borrowed) ctx_pinned_put(job->ctx, job->host);
+  if (job->host) ctx_pinned_put(job->ctx, job->host);
   delete job;
-}
-
-zkmi_msm_job* msm_job_replay(const zkmi_msm_job* cap, hipEvent_t done) {
-  zkmi_msm_job* j = new zkmi_msm_job(*cap);
-  j->done = done;
-  j->st = nullptr;  // its copy is finished by `done` (recorded after the graph launch)
-  j->borrowed = true;
-  return j;
-}
-void msm_job_release_captured(zkmi_msm_job* job) {
-  if (!job) return;
-  job->st = nullptr;  // the caller synchronised the context: no copy in flight
-  msm_job_free(job);
 }
 
 int msm_wait(zkmi_msm_job* job, uint64_t* out) {

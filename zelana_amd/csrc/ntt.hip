@@ -270,10 +270,7 @@ __device__ __forceinline__ Fe ntt_tab_scale(Fe v, uint64_t i, const NttIo& io) {
 // to hide the load and twiddle latency the 2-wave form exposes).
 
 template <bool DIT, int PRO, int EPI, bool PERM, int TB, int RB>
-#ifndef ZK_NTT_MINBLK
-#define ZK_NTT_MINBLK 4
-#endif
-__global__ void __launch_bounds__(256, (RB == 3 ? 2 : ZK_NTT_MINBLK)) k_ntt_group(const uint32_t* src, uint32_t* dst,
+__global__ void __launch_bounds__(256, (RB == 3 ? 2 : 4)) k_ntt_group(const uint32_t* src, uint32_t* dst,
                                                                           const uint32_t* __restrict__ tw, uint32_t logn,
                                                                           uint32_t a, uint32_t k, NttIo io) {
   constexpr int TILE = 1 << TB, EPT = 1 << RB;
@@ -528,27 +525,14 @@ static std::vector<uint32_t> ntt_groups(uint32_t logn) {
   return ks;
 }
 
-// group kernel shape: 1024-element radix-4 tiles (4 waves/SIMD; measured
-// 7% faster than the 2048-element radix-8 form); ZKMI_NTT_TB=11 selects the latter
-static int ntt_tb() {
-  static const int tb = [] {
-    const char* e = getenv("ZKMI_NTT_TB");
-    return e && atoi(e) == 11 ? 11 : 10;
-  }();
-  return tb;
-}
+// group kernel shape: 1024-element radix-4 tiles (4 waves/SIMD; measured 7%
+// faster than a 2048-element radix-8 form, which was dropped)
 template <bool DIT, int PRO, int EPI, bool PERM>
 static void launch_group(hipStream_t st, const uint32_t* src, uint32_t* dst, const uint32_t* tw, uint32_t logn,
                          uint32_t a, uint32_t k, const NttIo& io) {
-  if (ntt_tb() == 10) {
-    const size_t sm = (size_t)1024 * NL * 4;
-    const unsigned grid = (unsigned)((1ull << logn) / 1024);
-    k_ntt_group<DIT, PRO, EPI, PERM, 10, 2><<<grid, 256, sm, st>>>(src, dst, tw, logn, a, k, io);
-  } else {
-    const size_t sm = (size_t)NTT_TILE * NL * 4;
-    const unsigned grid = (unsigned)((1ull << logn) / NTT_TILE);
-    k_ntt_group<DIT, PRO, EPI, PERM, 11, 3><<<grid, 256, sm, st>>>(src, dst, tw, logn, a, k, io);
-  }
+  const size_t sm = (size_t)1024 * NL * 4;
+  const unsigned grid = (unsigned)((1ull << logn) / 1024);
+  k_ntt_group<DIT, PRO, EPI, PERM, 10, 2><<<grid, 256, sm, st>>>(src, dst, tw, logn, a, k, io);
 }
 
 // in-place transform in the requested order without scaling:

@@ -18,9 +18,6 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
-static std::atomic<uint64_t> g_graph_gen{1};
-uint64_t graph_gen() { return g_graph_gen.load(); }
-void graph_gen_bump() { g_graph_gen++; }
 
 int Workspace::get(const char* name, size_t bytes, void** out) {
   auto it = bufs.find(name);
@@ -28,7 +25,6 @@ int Workspace::get(const char* name, size_t bytes, void** out) {
     *out = it->second.first;
     return 0;
   }
-  graph_gen_bump();
   if (it != bufs.end()) {
     hipFree(it->second.first);
     bufs.erase(it);
@@ -45,7 +41,6 @@ int Workspace::get(const char* name, size_t bytes, void** out) {
   return 0;
 }
 void Workspace::release_all() {
-  graph_gen_bump();
   for (auto& kv : bufs) hipFree(kv.second.first);
   bufs.clear();
 }
@@ -171,7 +166,6 @@ void zkmi_ctx_destroy(zkmi_ctx* ctx) {
     hipStreamDestroy(l->st);
     delete l;
   }
-  prove_graphs_free(ctx);
   ctx->lanes.clear();
   if (ctx->prove_fork) hipEventDestroy(ctx->prove_fork);
   for (auto& pb : ctx->pinned_free) hipHostFree(pb.first);
@@ -209,7 +203,6 @@ int zkmi_dev_alloc(zkmi_ctx* ctx, size_t bytes, void** dptr) {
 }
 int zkmi_dev_free(zkmi_ctx* ctx, void* dptr) {
   ZK_DEVICE_GUARD(ctx);
-  graph_gen_bump();
   ZK_HIP(hipFree(dptr));
   return 0;
 }
@@ -242,9 +235,7 @@ int zkmi_bases_create_g2(zkmi_ctx* ctx, const uint64_t* affine, size_t n, zkmi_b
 void zkmi_bases_destroy(zkmi_bases* b) {
   ZK_DEVICE_GUARD(b);
   if (!b) return;
-  graph_gen_bump();
   hipFree(b->d_pts);
-  if (b->d_neg) hipFree(b->d_neg);
   delete b;
 }
 size_t zkmi_bases_len(const zkmi_bases* b) { return b ? b->n : 0; }
@@ -373,7 +364,6 @@ int zkmi_msm_set_lanes(zkmi_ctx* ctx, int lanes) {
     return ZKMI_EINVAL;
   }
   ctx->msm_lanes = lanes;
-  graph_gen_bump();
   return 0;
 }
 int zkmi_msm_set_window(zkmi_ctx* ctx, int c) {
@@ -382,7 +372,6 @@ int zkmi_msm_set_window(zkmi_ctx* ctx, int c) {
     return ZKMI_EINVAL;
   }
   ctx->msm_window = c;
-  graph_gen_bump();
   return 0;
 }
 int zkmi_g1_add(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {

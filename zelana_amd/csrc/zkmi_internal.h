@@ -31,11 +31,6 @@ void set_error(const char* fmt, ...);
   } while (0)
 
 // grow-only device scratch buffers keyed by name
-// Bumped whenever device memory a captured proof graph may point at is freed
-// or replaced (workspace growth, buffer / base-set / R1CS frees, window or lane
-// changes): graphs record it and are re-captured when it moved.
-uint64_t graph_gen();
-void graph_gen_bump();
 
 struct Workspace {
   std::map<std::string, std::pair<void*, size_t>> bufs;
@@ -81,8 +76,6 @@ struct zkmi_ctx {
   // of forking from the stream's current tail (groth16 small-proof schedule)
   hipEvent_t msm_fork = nullptr;
   hipEvent_t prove_fork = nullptr;  // owned: the event groth16_prove_submit uses for it
-  std::vector<void*> prove_graphs;  // zk::ProveGraph* (groth16.hip), freed by prove_graphs_free
-  bool graphs_off = false;          // a capture failed once: no more graphs on this context
 };
 
 struct zkmi_bases {
@@ -99,10 +92,6 @@ struct zkmi_bases {
   // 1: full table (tw = 1) with balanced window widths -- copy j is
   // 2^(offset of window j) * P_i, WinLayout<tc, true> in msm.hip
   int tbal = 0;
-  // The table again with every y negated (same layout), so the one-lane-per-
-  // bucket accumulation gathers -P for a negative digit instead of negating
-  // per entry; opt-in (ZKMI_NEG_TABLE=1, measured level), null otherwise.
-  uint32_t* d_neg = nullptr;
   // Window plans agreed with the other ranks of a communicator for this shard
   // (msm_submit_sharded): the first sharded MSM of a (communicator, n, table
   // state, window setting) runs the header all-gather, later ones reuse it.
@@ -220,12 +209,6 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out_affine);
 int msm_submit_shared(zkmi_ctx* ctx, const zkmi_bases* const* bs, int k, size_t offset, const void* d_scalars,
                       size_t n, zkmi_msm_job** jobs);
 void msm_job_free(zkmi_msm_job* job);
-// Proof-graph replays (groth16.hip): a job for the bit sums a captured job's
-// D2H writes into its (graph-owned) pinned buffer, finished by `done`.
-zkmi_msm_job* msm_job_replay(const zkmi_msm_job* captured, hipEvent_t done);
-// release a captured job: its pinned buffer back to the pool, no event
-void msm_job_release_captured(zkmi_msm_job* job);
-void prove_graphs_free(zkmi_ctx* ctx);
 int bases_upload(zkmi_ctx* ctx, int g2, const uint64_t* host_affine, size_t n, zkmi_bases** out);
 // convert canonical affine already in device memory (n points) into a bases set
 int bases_from_device_canon(zkmi_ctx* ctx, int g2, const uint32_t* d_canon, size_t n, zkmi_bases** out);
