@@ -186,37 +186,6 @@ ZK_HD Xyzz<FqOps> xyzz_madd_g1f(const Xyzz<FqOps>& p, const Fe& qx, const Fe& qy
   return r;
 }
 
-// xyzz_madd_g1f without the exceptional branch's use of Q: *special = 1 when
-// Q == P (the caller doubles Q, re-reading it), 2 when Q == -P (result at
-// infinity), 0 otherwise.  qx and qy are dead after their two products, which
-// keeps them out of the live set of the rest of the addition (the one-lane-per-
-// bucket accumulation's register peak; acc_items_g1l).
-ZK_HD Xyzz<FqOps> xyzz_madd_g1f_nd(const Xyzz<FqOps>& p, const Fe& qx, const Fe& qy, int* special) {
-  const Fe ny1 = bsub(FqP::B4_1, p.y);                            // 4p - Y1, limbs < 2^30
-  const Fe pp_ = mul_add<FqP>(qx, p.zz, bsub(FqP::B8_1, p.x));  // U2 - X1 + 8p
-  const Fe rr = mul_add<FqP>(qy, p.zzz, ny1);                    // S2 - Y1 + 4p
-  const Fe pp = sqr<FqP>(pp_);                                   // < 1.48p: == 0 mod p iff in {0, p}
-  uint32_t z = 0, e = 0;
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    z |= pp.v[i];
-    e |= pp.v[i] ^ FqP::P[i];
-  }
-  *special = 0;
-  if (z == 0 || e == 0) {  // U2 == X1: Q = +-P
-    *special = is_zero<FqP>(reduce_q32<FqP>(rr)) ? 1 : 2;
-    return p;
-  }
-  const Fe ppp = mul<FqP>(pp_, pp);
-  const Fe qq = mul<FqP>(p.x, pp);
-  Xyzz<FqOps> r;
-  r.x = sqr_add<FqP>(rr, bsub2(FqP::B6_3, ppp, qq));
-  r.y = mul2<FqP>(rr, bsubadd(FqP::B10_1, r.x, qq), ny1, ppp);
-  r.zz = mul<FqP>(p.zz, pp);
-  r.zzz = mul<FqP>(p.zzz, ppp);
-  return r;
-}
-
 // P + Q with both affine (mmadd-2008-s): xyzz_madd_g1 with ZZ1 = ZZZ1 = 1, so
 // U2 = x2, S2 = y2, ZZ3 = PP, ZZZ3 = PPP -- four products fewer (the second
 // entry of every bucket; the first is xyzz_from_aff).  Same field values as

@@ -47,17 +47,12 @@ namespace zk {
 // oldest-first issue arbitration: in a rocprofv3 trace of the 3-lane 2^20
 // pipeline the 12-us P1 count took 462 us and the scans 7 -> 48 us, and no
 // accumulation ran for 28% of the step.  The tails issue little VALU work, so
-// letting them win arbitration costs the accumulation little.
-#ifndef ZK_TAIL_PRIO
-#define ZK_TAIL_PRIO 3
-#endif
-#ifndef ZK_BR_MINW
-#define ZK_BR_MINW 1
-#endif
-#define ZK_TAIL_WAVE()                                        \
-  do {                                                        \
-    if (ZK_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(ZK_TAIL_PRIO); \
-  } while (0)
+// letting them win arbitration costs the accumulation little.  (Measured: the
+// P1 count no longer waits, 462 -> 12-28 us; the headline moved within noise,
+// because the 1024-thread P1 scatter and the 152-VGPR reductions still wait
+// for accumulation waves to retire -- a register / LDS footprint matter,
+// DESIGN.md §2.1.)
+#define ZK_TAIL_WAVE() __builtin_amdgcn_s_setprio(3)
 
 // ----------------------------------------------------------------- traits
 struct G1T {
@@ -477,82 +472,75 @@ __global__ void __launch_bounds__(T) k_rs_p1f_scatter(const uint32_t* __restrict
                                                           okey, oval);
 }
 
-// The same scatter with a small register footprint (256 threads, <= ~64
-// VGPRs): a thread holds only its W ranks; the digits are recomputed from the
-// scalar for the placement pass instead of being held across the block scan.
-// Small enough to run beside the accumulation kernel of another MSM lane
-// (its 3 waves per SIMD leave ~100 VGPRs), where the 1024-thread form needs a
-// whole empty CU.
+// Small sorts (<= SMALL_SORT_MAX entries: the small proofs' MSMs, ~10^5
+// entries over a few thousand buckets) are latency-bound: the two-pass radix
+// sort's ~11 launches cost ~180 us per MSM there.  Counting sort with global
+// atomics instead, in 3 launches: per-bucket counts (a thread per scalar and
+// its W digits), one workgroup's exclusive scan (bucket starts + a cursor
+// copy), and the scatter, whose positions come from atomics on the cursors.
+// Order inside a bucket is then arbitrary, as everywhere (group addition is
+// exact).  Contention stays low: ~30 entries per bucket.
+constexpr size_t SMALL_SORT_MAX = (size_t)1 << 18;
 template <int C, bool BAL>
-__global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_scatter_lr(const uint32_t* __restrict__ scalars, size_t n,
-                                                                  int Wp, uint32_t B, uint32_t NH, uint32_t lob,
-                                                                  uint32_t CS, uint32_t nc1,
-                                                                  const uint32_t* __restrict__ offs1,
-                                                                  uint32_t* __restrict__ okey,
-                                                                  uint32_t* __restrict__ oval) {
+__global__ void __launch_bounds__(256) k_ss_count(const uint32_t* __restrict__ scalars, size_t n, int Wp, uint32_t B,
+                                                  uint32_t* __restrict__ cnt) {
   ZK_TAIL_WAVE();
-  constexpr int T = RS_THREADS;
   constexpr int W = msm_windows(C);
-  extern __shared__ uint32_t lds[];
-  uint32_t* hist = lds;
-  uint32_t* lstart = lds + NH;
-  uint32_t* gbase = lds + 2 * NH;
-  uint32_t* tmp = lds + 3 * NH;
-  uint32_t* skey = tmp + T;
-  uint32_t* sv = skey + W * T;
-  for (uint32_t x = threadIdx.x; x < NH; x += T) {
-    gbase[x] = offs1[(size_t)x * nc1 + blockIdx.x];
-    hist[x] = 0;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t key[W], val[W];
+  bool ok[W];
+  rs_scalar_keys<C, BAL>(scalars, i, n, Wp, B, key, val, ok);
+#pragma unroll
+  for (int w = 0; w < W; w++)
+    if (ok[w]) atomicAdd(&cnt[key[w]], 1u);
+}
+// one 1024-thread workgroup: bstart[k] = sum of cnt[< k], bstart[K] = total,
+// cursor = a copy of bstart[0..K)
+__global__ void __launch_bounds__(1024) k_ss_scan(const uint32_t* __restrict__ cnt, uint32_t K,
+                                                  uint32_t* __restrict__ bstart, uint32_t* __restrict__ cursor) {
+  ZK_TAIL_WAVE();
+  __shared__ uint32_t wsum[16];
+  const uint32_t per = (K + 1023) / 1024, k0 = threadIdx.x * per, k1 = min(K, k0 + per);
+  uint32_t sum = 0;
+  for (uint32_t k = k0; k < k1; k++) sum += cnt[k];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= (unsigned)off) inc += t;
   }
+  if (lane == 63) wsum[wid] = inc;
   __syncthreads();
-  const size_t base = (size_t)blockIdx.x * CS;
-  const uint32_t cnt = (uint32_t)std::min<size_t>(CS, n - base);
-  const uint32_t nsub = (cnt + T - 1) / T;
-  for (uint32_t sub = 0; sub < nsub; sub++) {
-    const uint32_t k = sub * T + threadIdx.x;
-    const size_t i = base + k;
-    uint32_t rk[W];
-    {
-      int32_t d[W];
-      if (k < cnt) scalar_digits<C, BAL>(scalars, i, d);
+  uint32_t run = inc - sum, total = 0;
 #pragma unroll
-      for (int w = 0; w < W; w++) {
-        const int32_t v = k < cnt ? d[w] : 0;
-        const uint32_t wq = (uint32_t)(w % Wp);
-        if (v != 0) rk[w] = atomicAdd(&hist[(wq * B + (uint32_t)(v < 0 ? -v : v) - 1) >> lob], 1u);
-      }
-    }
-    __syncthreads();
-    const uint32_t total = rs_block_scan<T>(hist, lstart, NH, tmp);
-    __syncthreads();
-    if (k < cnt) {
-      int32_t d[W];
-      scalar_digits<C, BAL>(scalars, i, d);
-#pragma unroll
-      for (int w = 0; w < W; w++) {
-        const int32_t v = d[w];
-        if (v == 0) continue;
-        const uint32_t wq = (uint32_t)(w % Wp), j = (uint32_t)(w / Wp);
-        const uint32_t key = wq * B + (uint32_t)(v < 0 ? -v : v) - 1;
-        const uint32_t lp = lstart[key >> lob] + rk[w];
-        skey[lp] = key;
-        sv[lp] = (uint32_t)(j * n + i) | (v < 0 ? 0x80000000u : 0u);
-      }
-    }
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < total; q += T) {
-      const uint32_t kk = skey[q], bn = kk >> lob;
-      const uint32_t g = gbase[bn] + (q - lstart[bn]);
-      okey[g] = kk;
-      oval[g] = sv[q];
-    }
-    __syncthreads();
-    for (uint32_t x = threadIdx.x; x < NH; x += T) {
-      gbase[x] += hist[x];
-      hist[x] = 0;
-    }
-    __syncthreads();
+  for (int w = 0; w < 16; w++) {
+    const uint32_t tw = wsum[w];
+    if ((uint32_t)w < wid) run += tw;
+    total += tw;
   }
+  for (uint32_t k = k0; k < k1; k++) {
+    bstart[k] = run;
+    cursor[k] = run;
+    run += cnt[k];
+  }
+  if (threadIdx.x == 0) bstart[K] = total;
+}
+template <int C, bool BAL>
+__global__ void __launch_bounds__(256) k_ss_scatter(const uint32_t* __restrict__ scalars, size_t n, int Wp,
+                                                    uint32_t B, uint32_t* __restrict__ cursor,
+                                                    uint32_t* __restrict__ sval) {
+  ZK_TAIL_WAVE();
+  constexpr int W = msm_windows(C);
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t key[W], val[W];
+  bool ok[W];
+  rs_scalar_keys<C, BAL>(scalars, i, n, Wp, B, key, val, ok);
+#pragma unroll
+  for (int w = 0; w < W; w++)
+    if (ok[w]) sval[atomicAdd(&cursor[key[w]], 1u)] = val[w];
 }
 
 // one workgroup: bin starts and tile starts (tiles of <= C2 entries per bin)
@@ -1106,7 +1094,6 @@ __global__ void k_items_offsets(const uint32_t* __restrict__ hist, uint32_t cap,
     run += hist[cl];
   }
   nitems[0] = run;
-  nitems[2] = 0;  // work counter of the persistent accumulation (k_acc_items_g1p)
 }
 
 // Also resets the partial list the segmented cascade reads (xkey = no key,
@@ -1207,7 +1194,7 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
     v_nxt = v_nn;
     if (p + 2 < end) v_nn = sval[p + 2];
     const uint32_t* w = reinterpret_cast<const uint32_t*>(cr);
-    const bool binf = (w[G::PW - 1] >> 31) != 0;  // base at infinity: mode 3 (no `continue`, see acc_items_g1l)
+    const bool binf = (w[G::PW - 1] >> 31) != 0;  // base at infinity: mode 3 (no `continue`, see acc_items_g1f)
     Aff<F> P;
     const bool ng = (v >> 31) != 0;  // negative digit: negate y
     if constexpr (G::CW == 8) {
@@ -1269,7 +1256,10 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
   int phase = 0;  // 0: nothing yet, 1: acc is one affine point, 2: general
   auto step = [&](const uint4 (&r)[4], uint32_t v) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(r);
-    const int mode = (w[G1T::PW - 1] >> 31) ? 3 : phase;  // 3: base at infinity (see acc_items_g1l)
+    // 3: a base at infinity adds nothing.  Folded into the phase switch: a
+    // `return` / `continue` here cost the kernel 23 VGPRs (152 -> 129, i.e. 3
+    // waves/SIMD with room to spare; 2^20 3-lane 862-870 -> 873-899 Mpt/s)
+    const int mode = (w[G1T::PW - 1] >> 31) ? 3 : phase;
     const Fe x2 = unpack(w);
     const Fe y0 = unpack(w + 8);
     const Fe yn = bsub(FqP::B2_1, y0);
@@ -1334,138 +1324,12 @@ __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
   acc_items_g1f(items, nitems, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts,
                      blockIdx.x * blockDim.x + threadIdx.x);
 }
-// Persistent form: a grid of a few workgroups per CU whose waves take 64
-// items at a time from a counter (nitems[2], reset by k_items_offsets), in the
-// plan's longest-first order.  Launched with fewer waves per SIMD than the
-// kernel's VGPR budget allows, it leaves room for other lanes' sort and
-// bucket-reduction waves to run beside it.
-//
-// Rows come through LDS (global_load_lds_dwordx4, 1 KiB per wave-instruction,
-// lane-linear): the row of entry p + 1 lands in the wave's 4 KiB slot while
-// entry p is added, so no VGPRs hold a row in flight (acc_items_g1f keeps 16).
-// With <= 128 VGPRs three waves per SIMD leave a quarter of the register file
-// to the tail kernels of other lanes (sort, piece sums, bucket reduction), which
-// then run beside the accumulation instead of waiting for it to drain.
-typedef __attribute__((address_space(1))) void zk_gvoid;
-typedef __attribute__((address_space(3))) void zk_lvoid;
-// s_waitcnt encodings (gfx9: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
-constexpr int ZK_WAIT_VM0 = 0x0F70;
-constexpr int ZK_WAIT_LGKM0 = 0xC07F;
-__device__ __forceinline__ void acc_items_g1l(const uint4* __restrict__ items, uint32_t total,
-                                              const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                                              uint32_t tn, uint32_t tskip,
-                                              uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey,
-                                              uint32_t* __restrict__ xvalid, uint32_t* __restrict__ xpts,
-                                              uint32_t i, uint4 (*slot)[64]) {
-  using F = FqOps;
-  constexpr int XW = 32;
-  if (i >= total) return;
-  const int lane = threadIdx.x & 63;
-  const uint4 it = items[i];
-  const uint32_t start = it.x, end = it.y;
-  auto fetch = [&](uint32_t v) {  // row of entry value v -> this lane's slot (async)
-    uint32_t idx = v & 0x7FFFFFFFu;
-    if (tskip) idx += (idx / tn) * tskip;
-    const uint32_t* src = bases;
-    const uint4* q = reinterpret_cast<const uint4*>(src + (size_t)idx * G1T::PW);
-#pragma unroll
-    for (int k = 0; k < 4; k++) __builtin_amdgcn_global_load_lds((zk_gvoid*)(q + k), (zk_lvoid*)&slot[k][0], 16, 0, 0);
-  };
-  Xyzz<F> acc = xyzz_inf<F>();
-  int phase = 0;  // 0: nothing yet, 1: acc is one affine point, 2: general
-  const uint32_t last = end - 1;
-  uint32_t v_nxt = sval[start];
-  fetch(v_nxt);
-  uint32_t v_nn = sval[min(start + 1, last)];
-  for (uint32_t p = start; p < end; p++) {
-    const uint32_t v = v_nxt;
-    __builtin_amdgcn_s_waitcnt(ZK_WAIT_VM0);  // this lane's row has landed
-    uint4 cr[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) cr[k] = slot[k][lane];
-    __builtin_amdgcn_s_waitcnt(ZK_WAIT_LGKM0);  // read before the next row overwrites the slot
-    fetch(v_nn);  // unconditional: past the end it re-reads the last entry
-    v_nxt = v_nn;
-    v_nn = sval[min(p + 2, last)];
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(cr);
-    // a base at infinity adds nothing: folded into the phase switch (a
-    // `continue` here cost 34 VGPRs: 145 -> 111)
-    const int mode = (w[G1T::PW - 1] >> 31) ? 3 : phase;
-    const Fe x2 = unpack(w);
-    const Fe y0 = unpack(w + 8);
-    const Fe yn = bsub(FqP::B2_1, y0);
-    const bool ng = (v >> 31) != 0;
-    Fe y2;
-#pragma unroll
-    for (int k = 0; k < NL; k++) y2.v[k] = ng ? yn.v[k] : y0.v[k];
-    if (mode == 2) {
-      int special;
-      acc = xyzz_madd_g1f_nd(acc, x2, y2, &special);
-      if (special == 2) {
-        phase = 0;
-      } else if (special == 1) {  // Q == P (rare): re-read Q and double it
-        uint32_t idx = v & 0x7FFFFFFFu;
-        if (tskip) idx += (idx / tn) * tskip;
-        const uint32_t* src = bases;
-        const uint32_t* q = src + (size_t)idx * G1T::PW;
-        const Fe qy0 = unpack(q + 8);
-        const Fe qy = ng ? bsub(FqP::B2_1, qy0) : qy0;
-        acc = xyzz_mdbl(Aff<F>{unpack(q), reduce_q32<FqP>(qy)});
-      }
-    } else if (mode == 1) {
-      acc = xyzz_mmadd_g1({acc.x, acc.y}, Aff<F>{x2, reduce_q32<FqP>(y2)});
-      phase = xyzz_is_inf(acc) ? 0 : 2;
-    } else if (mode == 0) {
-      acc = xyzz_from_aff(Aff<F>{x2, reduce_q32<FqP>(y2)});
-      phase = 1;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(ZK_WAIT_VM0);  // the last (redundant) row lands before the slot is reused
-  if (phase == 0) acc = xyzz_inf<F>();
-  if (it.w == NOSLOT) {
-    st_acc<G1T>(buckets + (size_t)it.z * XW, acc);
-  } else {
-    xkey[it.w] = it.z;
-    xvalid[it.w] = 1;
-    st_acc<G1T>(xpts + (size_t)it.w * XW, acc);
-  }
-}
-// One 768-thread workgroup per CU (grid = CUs): 12 waves = exactly 3 per
-// SIMD whatever the kernel's register count, so the rest of every SIMD's
-// register file (512 - 3 x 120 = 152 VGPRs) and 112 KiB of LDS stay free for
-// the tails of the other lanes.  (768 workgroups of 256 threads did not land 3
-// per CU: at 113 VGPRs the dispatcher packs 4 on some CUs and leaves others
-// empty.)
-constexpr int ACCP_THREADS = 768;
-__global__ void __launch_bounds__(ACCP_THREADS)
-    k_acc_items_g1p(const uint4* __restrict__ items, uint32_t* __restrict__ nitems,
-                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                    uint32_t tn, uint32_t tskip,
-                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                    uint32_t* __restrict__ xpts) {
-  __shared__ uint4 rows[ACCP_THREADS / 64][4][64];  // per wave: 4 x 1 KiB, lane-linear
-  const uint32_t total = nitems[0];
-  const int lane = threadIdx.x & 63;
-  for (;;) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&nitems[2], 64u);
-    base = (uint32_t)__shfl((int)base, 0, 64);
-    if (base >= total) break;
-    acc_items_g1l(items, total, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts, base + lane,
-                  rows[threadIdx.x >> 6]);
-  }
-}
-// one item per thread, rows through LDS (A/B against k_acc_items_g1)
-__global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
-    k_acc_items_g1l(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
-                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                    uint32_t tn, uint32_t tskip,
-                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                    uint32_t* __restrict__ xpts) {
-  __shared__ uint4 rows[4][4][64];
-  acc_items_g1l(items, nitems[0], sval, bases, tn, tskip, buckets, xkey, xvalid, xpts,
-                blockIdx.x * blockDim.x + threadIdx.x, rows[threadIdx.x >> 6]);
-}
+// (Tried for the 3-lane pipeline: rows staged through LDS by
+// global_load_lds, and a persistent form with one 768-thread workgroup per CU
+// (3 waves/SIMD, the rest of the register file left to other lanes' tails):
+// the tails then ran beside the accumulation (95-100% of the step with an
+// accumulation running) but the accumulation itself slowed by as much:
+// 2^20 3-lane 1.24-1.29 ms/step against 1.17-1.20; dropped.)
 __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
     k_acc_items_g2(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
@@ -1478,7 +1342,7 @@ __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
 // Buckets split into 2..ITEM_SEQ_MAX pieces: one thread sums them (contiguous
 // partial slots) and invalidates them; longer ones stay for k_msm_accN.
 template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, 8))) k_items_combine(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
+__global__ void __launch_bounds__(256) k_items_combine(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
                                                        const uint32_t* __restrict__ pbase,
                                                        uint32_t* __restrict__ buckets, uint32_t* __restrict__ xvalid,
                                                        const uint32_t* __restrict__ xpts,
@@ -1502,7 +1366,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_
 }
 
 template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, 8))) k_msm_accN(const uint32_t* __restrict__ xkey, const uint32_t* __restrict__ xvalid,
+__global__ void __launch_bounds__(256) k_msm_accN(const uint32_t* __restrict__ xkey, const uint32_t* __restrict__ xvalid,
                                                   const uint32_t* __restrict__ xpts, uint32_t M, uint32_t L,
                                                   uint32_t nchunks, uint32_t* __restrict__ buckets,
                                                   uint32_t* __restrict__ ykey, uint32_t* __restrict__ yvalid,
@@ -1666,12 +1530,10 @@ __global__ void __launch_bounds__(256) k_msm_accN_coop(const uint32_t* __restric
 __device__ __forceinline__ uint32_t insert_bit(uint32_t t, int bit) {
   return (((t >> bit) << (bit + 1)) | (1u << bit) | (t & ((1u << bit) - 1)));
 }
-#ifndef ZK_BR_WPE
-#define ZK_BR_WPE 4
-#endif
+#define ZK_BR_WPE 4  // at most 4 waves/SIMD: the compiler may use up to 128 VGPRs
 
 template <class G, bool BITS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE))) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
                                                 const uint32_t* __restrict__ bstart, int lb, int hb, int W, int sr,
                                                 int sc, int sb, int segt, uint32_t* __restrict__ out0,
                                                 uint32_t* __restrict__ out1) {
@@ -1784,7 +1646,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_
 // jobs (4 folds + 6 levels each), and the bucket reduction runs beside the
 // other lane's accumulation, where wasted VALU issue is what it costs.
 template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE))) k_msm_br_strip(const uint32_t* __restrict__ buckets,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br_strip(const uint32_t* __restrict__ buckets,
                                                       const uint32_t* __restrict__ bstart, int lb, int hb, int W,
                                                       int sr, int sc, int mc, uint32_t* __restrict__ outC,
                                                       uint32_t* __restrict__ outD) {
@@ -2437,15 +2299,8 @@ static void launch_p1_fused(hipStream_t st, const uint32_t* sc, size_t n, int Wp
   // sub-tiles of 1024 scalars when their LDS fits (c >= 15: W <= 17), else
   // 256: 2^26 table MSM sort 12.2 -> 10.4 ms isolated (P1 runs 6 -> 24
   // entries per bin; tools/rs_ab.sh)
-  static const int env_t1 = [] {
-    const char* e = getenv("ZKMI_RS_T1");
-    return e ? atoi(e) : 1024;
-  }();
   constexpr int W = msm_windows(C);
-  if (scatter && env_t1 == 2)  // low-register 256-thread form (co-resides with an accumulation)
-    k_rs_p1f_scatter_lr<C, BAL><<<nf, RS_THREADS, rs_scatter_lds(NH, RS_THREADS * W), st>>>(
-        sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval);
-  else if (scatter && env_t1 == 1024 && rs_scatter_lds(NH, 1024 * W, 1024) <= 160 * 1024)
+  if (scatter && rs_scatter_lds(NH, 1024 * W, 1024) <= 160 * 1024)
     k_rs_p1f_scatter<C, 1024, BAL><<<nf, 1024, rs_scatter_lds(NH, 1024 * W, 1024), st>>>(sc, n, Wp, B, NH, lob, CS, nf,
                                                                                     cnt1, okey, oval);
   else if (scatter)
@@ -2467,6 +2322,31 @@ static int p1_fused(int c, bool bal, hipStream_t st, const uint32_t* sc, size_t 
 #undef ZK_C
     default:
       set_error("p1_fused: unsupported MSM window %d", c);
+      return ZKMI_EINVAL;
+  }
+  return 0;
+}
+
+template <int C, bool BAL>
+static void launch_small_sort(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t K,
+                              uint32_t* cnt, uint32_t* cursor, uint32_t* bstart, uint32_t* sval) {
+  const unsigned g = (unsigned)((n + 255) / 256);
+  k_ss_count<C, BAL><<<g, 256, 0, st>>>(sc, n, Wp, B, cnt);
+  k_ss_scan<<<1, 1024, 0, st>>>(cnt, K, bstart, cursor);
+  k_ss_scatter<C, BAL><<<g, 256, 0, st>>>(sc, n, Wp, B, cursor, sval);
+}
+static int small_sort(int c, bool bal, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t K,
+                      uint32_t* cnt, uint32_t* cursor, uint32_t* bstart, uint32_t* sval) {
+  switch (c) {
+#define ZK_C(CC)                                                                     \
+  case CC:                                                                           \
+    if (bal) launch_small_sort<CC, true>(st, sc, n, Wp, B, K, cnt, cursor, bstart, sval); \
+    else launch_small_sort<CC, false>(st, sc, n, Wp, B, K, cnt, cursor, bstart, sval);    \
+    break;
+    ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15) ZK_C(16) ZK_C(17) ZK_C(18) ZK_C(19) ZK_C(20) ZK_C(21) ZK_C(22)
+#undef ZK_C
+    default:
+      set_error("small_sort: unsupported MSM window %d", c);
       return ZKMI_EINVAL;
   }
   return 0;
@@ -2578,19 +2458,16 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   // lo digit = the rest (8..13 bits) inside each hi bin (P2, XCD-local)
   uint32_t kb = 0;
   while ((1u << kb) < P.K) kb++;
-  static const int env_lob = [] { const char* e = getenv("ZKMI_RS_LOB"); return e ? atoi(e) : 0; }();
-  static const int env_c2 = [] { const char* e = getenv("ZKMI_RS_C2"); return e ? atoi(e) : 0; }();
   // 21-bit keys (c = 22 tables): 10 hi bits, 11 lo (2^26 with the 1024-thread
   // scatters: sort 10.5 -> 9.4 ms vs 9 + 12, 13.2 ms for 8 + 13; tools/rs_lob.sh)
-  const uint32_t lob = env_lob ? (uint32_t)env_lob : (kb > 20 ? kb - 10 : kb > 16 ? kb - 8 : 8);
+  const uint32_t lob = kb > 20 ? kb - 10 : kb > 16 ? kb - 8 : 8;
   const uint32_t NH = (P.K + (1u << lob) - 1) >> lob;
   const size_t Mmax = P.Mmax;
   // radix-sort geometry (see k_rs_*): ~2K P1 chunks, ~8K P2 tiles at most
   const uint32_t C1 = 16384u * (uint32_t)std::max<size_t>(1, (Mmax + 16384ull * 2048 - 1) / (16384ull * 2048));
   const uint32_t nc1 = (uint32_t)((Mmax + C1 - 1) / C1);
   const uint32_t C2b = std::max(8192u, 4u << lob);  // >= 4 entries per lo bin per tile
-  const uint32_t C2 = env_c2 ? (uint32_t)env_c2
-                            : C2b * (uint32_t)std::max<size_t>(1, (Mmax + (size_t)C2b * 8192 - 1) / ((size_t)C2b * 8192));
+  const uint32_t C2 = C2b * (uint32_t)std::max<size_t>(1, (Mmax + (size_t)C2b * 8192 - 1) / ((size_t)C2b * 8192));
   const uint32_t T2max = (uint32_t)((Mmax + C2 - 1) / C2) + NH;
   // fused P1: chunks of CS scalars (~2K chunks at most)
   const uint32_t CS = 1024u * (uint32_t)std::max<size_t>(1, (n + 1024ull * 2048 - 1) / (1024ull * 2048));
@@ -2624,6 +2501,19 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   }
   lane->debug_sorted = 1;
   ScopedKernelTimer tm(ctx, "msm_sort", st);
+  if (fused && Mmax <= SMALL_SORT_MAX) {
+    uint32_t *scnt, *scur;
+    ZK_TRY(ws.get("msm_ss_cnt", (size_t)P.K * 4, (void**)&scnt));
+    ZK_TRY(ws.get("msm_ss_cursor", (size_t)P.K * 4, (void**)&scur));
+    ZK_HIP(hipMemsetAsync(scnt, 0, (size_t)P.K * 4, st));
+    ZK_TRY(small_sort(P.c, P.bal, st, d_scalars, n, P.W, P.B, P.K, scnt, scur, bstart, sval));
+    ZK_HIP(hipEventRecord(lane->consumed, st));
+    ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
+    ZK_HIP(hipGetLastError());
+    *out_sval = sval;
+    *out_bstart = bstart;
+    return 0;
+  }
   if (!fused) {
     ZK_TRY(dispatch_digits(P.c, st, d_scalars, n, P.p, P.W, P.bal, digits));
     ZK_HIP(hipEventRecord(lane->consumed, st));
@@ -2635,11 +2525,6 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
     k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, total);
     k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
   };
-  static const int env_st1 = [] { const char* e = getenv("ZKMI_RS_ST1"); return e ? atoi(e) : 4096; }();
-  static const int env_st2 = [] { const char* e = getenv("ZKMI_RS_ST2"); return e ? atoi(e) : 0; }();
-  // P2 sub-tiles of 8192 entries (runs twice as long per lo bin; with 256
-  // threads they paid off only for >= 2^26 entries, with 1024 for all sizes)
-  const int st2 = env_st2 ? env_st2 : 8192;
   const uint32_t ne = (uint32_t)P.ne;
   if (fused) {
     ZK_TRY(p1_fused(P.c, P.bal, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, nullptr, nullptr, false));
@@ -2650,12 +2535,8 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   } else {
     k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1, cnt1);
     scan(cnt1, len1, &tot[0]);
-    if (env_st1 == 8192 && rs_scatter_lds(NH, 8192) <= 160 * 1024)
-    k_rs_p1_scatter<8192><<<nc1, RS_THREADS, rs_scatter_lds(NH, 8192), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1,
-                                                                               cnt1, okey, oval);
-  else
     k_rs_p1_scatter<4096><<<nc1, RS_THREADS, rs_scatter_lds(NH, 4096), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1,
-                                                                               cnt1, okey, oval);
+                                                                             cnt1, okey, oval);
   }
   k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, fused ? nf : nc1, NH, &tot[0], C2, binstart, tstart);
   // cnt2 needs no clearing: tiles t < tstart[NH] write all their counts, and
@@ -2664,18 +2545,14 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   k_rs_p2_count<<<g2, RS_THREADS, (1u << lob) * 4, st>>>(okey, binstart, tstart, NH, lob, C2, T2max, cnt2);
   scan(cnt2, len2, &tot[1]);
   k_rs_bstart<<<(P.K + 256) / 256, 256, 0, st>>>(cnt2, binstart, tstart, NH, lob, P.K, bstart);
-  // 1024-thread P2 workgroups over 8192-entry sub-tiles (2^20 table MSM, 3
-  // lanes, interleaved repeats: 1.344 -> 1.297 ms with the 1024-thread P1;
-  // tools/rs_ab2.sh)
-  static const int env_t2 = [] { const char* e = getenv("ZKMI_RS_T2"); return e ? atoi(e) : 1024; }();
   const uint32_t NLO = 1u << lob;
+  // 1024-thread P2 workgroups over 8192-entry sub-tiles (runs twice as long
+  // per lo bin as 4096; 2^20 table MSM, 3 lanes: 1.344 -> 1.297 ms with the
+  // 1024-thread P1; tools/rs_ab2.sh)
 #define ZK_P2(ST, T) \
   k_rs_p2_scatter<ST, T><<<g2, T, rs_scatter_lds(NLO, ST, T), st>>>(okey, oval, binstart, tstart, NH, lob, C2, T2max, cnt2, sval)
-  if (env_t2 == 1024 && st2 == 16384 && rs_scatter_lds(NLO, 16384, 1024) <= 160 * 1024) ZK_P2(16384, 1024);
-  else if (env_t2 == 1024 && st2 >= 8192 && rs_scatter_lds(NLO, 8192, 1024) <= 160 * 1024) ZK_P2(8192, 1024);
-  else if (env_t2 == 1024) ZK_P2(4096, 1024);
-  else if (st2 == 8192 && rs_scatter_lds(NLO, 8192) <= 160 * 1024) ZK_P2(8192, RS_THREADS);
-  else ZK_P2(4096, RS_THREADS);
+  if (rs_scatter_lds(NLO, 8192, 1024) <= 160 * 1024) ZK_P2(8192, 1024);
+  else ZK_P2(4096, 1024);
 #undef ZK_P2
   ZK_HIP(hipGetLastError());
   *out_sval = sval;
@@ -2819,23 +2696,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     {
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
       auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
-      static const int pers = [] {  // workgroups per CU of the persistent G1 form (0: one item per thread)
-        const char* e = getenv("ZKMI_ACC_PERS");
-        return e ? atoi(e) : 0;
-      }();
-      static const int lds = [] {
-        const char* e = getenv("ZKMI_ACC_LDS");
-        return e ? atoi(e) : 0;
-      }();
-      if (G::CW == 8 && lds && pers == 0)
-        k_acc_items_g1l<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases,
-                                                                            tn, tskip, buckets, xkey,
-                                                                            xvalid, xpts);
-      else if (G::CW == 8 && pers > 0)
-        k_acc_items_g1p<<<(unsigned)(ctx->num_cus * pers), ACCP_THREADS, 0, st>>>(items, &nitems[0], sval, d_bases,
-                                                                        tn, tskip, buckets, xkey, xvalid, xpts);
-      else
-        kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, tn,
+      kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, tn,
                                                                  tskip, buckets, xkey, xvalid, xpts);
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);
