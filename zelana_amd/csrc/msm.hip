@@ -2298,7 +2298,7 @@ static void launch_p1_fused(hipStream_t st, const uint32_t* sc, size_t n, int Wp
                             bool scatter) {
   // sub-tiles of 1024 scalars when their LDS fits (c >= 15: W <= 17), else
   // 256: 2^26 table MSM sort 12.2 -> 10.4 ms isolated (P1 runs 6 -> 24
-  // entries per bin; tools/rs_ab.sh)
+  // entries per bin)
   constexpr int W = msm_windows(C);
   if (scatter && rs_scatter_lds(NH, 1024 * W, 1024) <= 160 * 1024)
     k_rs_p1f_scatter<C, 1024, BAL><<<nf, 1024, rs_scatter_lds(NH, 1024 * W, 1024), st>>>(sc, n, Wp, B, NH, lob, CS, nf,
@@ -2381,7 +2381,8 @@ static int get_lane(zkmi_ctx* ctx, MsmLane** out) {
     MsmLane* l = new MsmLane;
     if (hipStreamCreateWithFlags(&l->st, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&l->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&l->consumed, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&l->consumed, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&l->acc_done, hipEventDisableTiming) != hipSuccess) {
       (void)hipGetLastError();
       delete l;
       set_error("msm: cannot create a stream / events for an MSM lane");
@@ -2693,12 +2694,25 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       k_items_offsets<<<1, 1, 0, st>>>(hist, cap, cursor, &nitems[0]);
       k_items_scatter<<<ig, 256, 0, st>>>(bstart, K, cap, hv, cursor, items, &flags[0], xkey, xvalid, (uint32_t)xl);
     }
+    // Table accumulations start in submission order across lanes: this one
+    // waits for the previous one (on another lane) to end.  Run together, two
+    // accumulations share the CUs and end together, and the lanes' tails and
+    // sorts then queue up behind both; chained, the earlier MSM's tail starts
+    // a full accumulation sooner.  Measured (interleaved, one box): bench
+    // headline 822-825 -> 832-840 Mpt/s, configs[0] resident 2.82-2.86 ->
+    // 2.78-2.80 ms, 2^20 / 2^26 loops and the proof legs level.  (Also chaining the bucket
+    // reduction, with 256-thread sorts that fit beside the accumulation:
+    // 2^26 steady state 64.5 -> 62 ms per MSM, but the accumulation ran 13%
+    // longer beside the sort, short runs lost and 2^20 lost 8%.)
+    if (ctx->acc_last && ctx->acc_last != lane) ZK_HIP(hipStreamWaitEvent(st, ctx->acc_last->acc_done, 0));
     {
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
       auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
       kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, tn,
                                                                  tskip, buckets, xkey, xvalid, xpts);
     }
+    ZK_HIP(hipEventRecord(lane->acc_done, st));
+    ctx->acc_last = lane;
     ScopedKernelTimer tm(ctx, "msm_accN", st);
     k_items_combine<GB><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, buckets, xvalid, xpts, &nitems[1]);
     ZK_HIP(hipGetLastError());

@@ -163,6 +163,7 @@ void zkmi_ctx_destroy(zkmi_ctx* ctx) {
     l->ws.release_all();
     hipEventDestroy(l->fork);
     hipEventDestroy(l->consumed);
+    hipEventDestroy(l->acc_done);
     hipStreamDestroy(l->st);
     delete l;
   }

@@ -45,6 +45,7 @@ struct MsmLane {
   hipStream_t st = nullptr;
   Workspace ws;
   hipEvent_t fork = nullptr, consumed = nullptr;
+  hipEvent_t acc_done = nullptr;  // end of this lane's last table accumulation (msm.hip acc chain)
   int debug_sorted = 0;  // ZKMI_DEBUG_SKIP ablations only (msm.hip)
 };
 
@@ -75,6 +76,9 @@ struct zkmi_ctx {
   // set: MSM lanes wait on this event (recorded earlier on `stream`) instead
   // of forking from the stream's current tail (groth16 small-proof schedule)
   hipEvent_t msm_fork = nullptr;
+  // the lane whose table accumulation was queued last: the next one (on another
+  // lane) starts after it (msm.hip msm_acc_phase)
+  zk::MsmLane* acc_last = nullptr;
   hipEvent_t prove_fork = nullptr;  // owned: the event groth16_prove_submit uses for it
 };
 
