@@ -183,6 +183,65 @@ __device__ __forceinline__ Fe sqr_ilp(const Fe& a) {
   return r;
 }
 
+// (a0 b0 + a1 b1 + a2 b2) R^-1 with ONE reduction (a Poseidon MDS row): the
+// three products share the m digits and the m*p columns, ~160 mads fewer than
+// three mul_ilp.  a_k < p (constants), b_k < 2p, normalised: the sum is
+// < 6 p^2, inside the Montgomery bound (R / p = 169), so the output is < 2p;
+// accumulator sums stay below 14 * 2^58 per column.
+__device__ __forceinline__ Fe mul3_ilp(const Fe& a0, const Fe& b0, const Fe& a1, const Fe& b1, const Fe& a2,
+                                       const Fe& b2) {
+  uint32_t m[NL];
+  Fe r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    uint64_t s0 = c, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int j = 0; j <= k; j++) {
+      if (j & 1) {
+        s1 += (uint64_t)a0.v[j] * b0.v[k - j];
+        s1 += (uint64_t)a1.v[j] * b1.v[k - j];
+        s3 += (uint64_t)a2.v[j] * b2.v[k - j];
+      } else {
+        s0 += (uint64_t)a0.v[j] * b0.v[k - j];
+        s0 += (uint64_t)a1.v[j] * b1.v[k - j];
+        s2 += (uint64_t)a2.v[j] * b2.v[k - j];
+      }
+      if (j < k) {
+        if (j & 1) s3 += (uint64_t)m[j] * FrP::P[k - j];
+        else s2 += (uint64_t)m[j] * FrP::P[k - j];
+      }
+    }
+    uint64_t tot = (s0 + s1) + (s2 + s3);
+    m[k] = ((uint32_t)tot * FrP::PINV) & LMASK;
+    tot += (uint64_t)m[k] * FrP::P[0];
+    c = tot >> 29;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+    uint64_t s0 = c, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+    for (int j = k - (NL - 1); j < NL; j++) {
+      if (j & 1) {
+        s1 += (uint64_t)a0.v[j] * b0.v[k - j];
+        s1 += (uint64_t)a1.v[j] * b1.v[k - j];
+        s3 += (uint64_t)a2.v[j] * b2.v[k - j];
+        s3 += (uint64_t)m[j] * FrP::P[k - j];
+      } else {
+        s0 += (uint64_t)a0.v[j] * b0.v[k - j];
+        s0 += (uint64_t)a1.v[j] * b1.v[k - j];
+        s2 += (uint64_t)a2.v[j] * b2.v[k - j];
+        s2 += (uint64_t)m[j] * FrP::P[k - j];
+      }
+    }
+    const uint64_t tot = (s0 + s1) + (s2 + s3);
+    r.v[k - NL] = (uint32_t)tot & LMASK;
+    c = tot >> 29;
+  }
+  r.v[NL - 1] = (uint32_t)c;
+  return r;
+}
+
 __device__ __forceinline__ void st_canon(uint32_t* z, uint32_t var, const Fe& v) {
   uint32_t w[8];
   pack(w, reduce<FrP>(v));
@@ -288,7 +347,7 @@ __device__ __forceinline__ void poseidon_quad(const Fe& in, uint32_t q, uint32_t
     }
     const Fe b0 = quad_bcast<0>(u), b1 = quad_bcast<1>(u), b2 = quad_bcast<2>(u);
     const Fe* row = pc + 3 * POS_ROUNDS + 3 * qq;
-    s = add<FrP>(add<FrP>(mul_ilp(row[0], b0), mul_ilp(row[1], b1)), mul_ilp(row[2], b2));
+    s = mul3_ilp(row[0], b0, row[1], b1, row[2], b2);
   }
 }
 
