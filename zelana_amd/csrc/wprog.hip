@@ -351,6 +351,43 @@ __device__ __forceinline__ void poseidon_quad(const Fe& in, uint32_t q, uint32_t
   }
 }
 
+// a^e (Montgomery form) for the Fermat inversion, on one lane: fixed 3-bit
+// windows over e (86 digits, table a^1..a^7 selected without dynamic
+// register indexing) with the latency-split products above -- ~74 products
+// and 253 squarings instead of the binary ladder's ~127 and 255 asm-chain
+// ones (the INV ops run alone on a lane, so latency is what counts).
+__device__ Fe pow_w3(const Fe& a, const uint64_t e[4]) {
+  Fe t[8];
+  t[1] = a;
+  t[2] = sqr_ilp(a);
+#pragma unroll
+  for (int k = 3; k < 8; k++) t[k] = mul_ilp(t[k - 1], a);
+  Fe r = fe_zero();
+  bool started = false;
+  for (int j = 85; j >= 0; j--) {
+    const int b0 = 3 * j;
+    uint32_t d = 0;
+#pragma unroll
+    for (int u = 2; u >= 0; u--) {
+      const int bit = b0 + u;
+      d = (d << 1) | (bit < 256 ? (uint32_t)((e[bit >> 6] >> (bit & 63)) & 1) : 0u);
+    }
+    if (started) {
+      r = sqr_ilp(r);
+      r = sqr_ilp(r);
+      r = sqr_ilp(r);
+    }
+    if (d) {
+      Fe m = t[1];
+#pragma unroll
+      for (int k = 2; k < 8; k++) m = sel(d == (uint32_t)k, t[k], m);
+      r = started ? mul_ilp(r, m) : m;
+      started = true;
+    }
+  }
+  return started ? r : one<FrP>();
+}
+
 // One op of a level, on the quad of lanes (op_i, q).
 template <bool POS>
 __device__ __forceinline__ void wprog_op(uint32_t op_i, uint32_t q, const uint4* __restrict__ ops,
@@ -417,7 +454,7 @@ __device__ __forceinline__ void wprog_op(uint32_t op_i, uint32_t q, const uint4*
     const uint64_t e[4] = {0x43e1f593efffffffULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL,
                            0x30644e72e131a029ULL};
     const Fe am = mul<FrP>(a, fe_const<FrP>(FrP::R2));
-    Fe inv = redc_fr(reduce<FrP>(pow<FrP>(am, e)));
+    Fe inv = redc_fr(reduce<FrP>(pow_w3(am, e)));
     if (kind == WP_INV1) {
       uint32_t nz = 0;
 #pragma unroll
