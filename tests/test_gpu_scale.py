@@ -183,6 +183,29 @@ def test_msm_2pow20_table_plan_matches_oracle(ctx):
         ctx.set_lanes(2)
 
 
+def test_msm_lanes_distinct_inputs_in_flight(ctx):
+    """Table MSMs with different scalars in flight on three lanes, whose
+    accumulations are chained across lanes (msm.hip msm_acc_phase), each
+    equal the same MSM run alone: no lane reads another lane's sort, items or
+    buckets.  Two base sets alternate so consecutive lanes also switch
+    tables; c = 20 puts them on the one-lane-per-bucket (chained) path."""
+    n = 1 << 18
+    sets = [ctx.bases_generate(seed=1020 + k, n=n) for k in range(2)]
+    for b in sets:
+        assert b.precompute(c=20)[1] == 20
+    scal = [ctx.scalars_generate(seed=40 + i, n=n) for i in range(6)]
+    ctx.set_lanes(1)
+    alone = [ctx.msm(sets[i % 2], scal[i]) for i in range(6)]
+    ctx.set_lanes(3)
+    try:
+        jobs = [ctx.msm_submit(sets[i % 2], scal[i], n) for i in range(6)]
+        for i, j in enumerate(jobs):
+            assert np.array_equal(ctx.msm_wait(j), alone[i]), i
+    finally:
+        ctx.set_lanes(2)
+    assert not np.array_equal(alone[0], alone[1])
+
+
 def test_msm_2pow26_table_plan_matches_oracle(ctx):
     """Config 5 at its full size: one 2^26 MSM over the
     c = 22, 12-copy table, as one GPU runs it (bench.py extra.msm_global_2_26,
