@@ -138,8 +138,14 @@ int zkmi_msm_submit_shared(zkmi_ctx* ctx, const zkmi_bases* const* bs, int k, si
                            size_t n, zkmi_msm_job** jobs);
 int zkmi_msm_set_window(zkmi_ctx* ctx, int c);
 /* Number of MSM lanes (streams with their own scratch) used round-robin by
- * consecutive submissions so their latency-bound tails overlap; 1..8. */
+ * consecutive submissions so their latency-bound tails overlap; 1..8, at most
+ * 2 while a communicator exists on the context (stream budget, below). */
 int zkmi_msm_set_lanes(zkmi_ctx* ctx, int lanes);
+/* lanes in effect (after the communicator cap) */
+int zkmi_msm_get_lanes(const zkmi_ctx* ctx);
+/* streams the library holds for this context (context stream, MSM lanes,
+ * communicator and witness-program streams) */
+int zkmi_ctx_stream_count(const zkmi_ctx* ctx);
 
 /* canonical affine point arithmetic helpers (host) */
 int zkmi_g1_add(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
@@ -164,9 +170,18 @@ int zkmi_g2_add(const uint64_t a[16], const uint64_t b[16], uint64_t out[16]);
  *   zkmi_comm_init_host  the host supplies the all-gather (MPI, a TCP store,
  *                        pipes ...): for hosts without RCCL, or ranks that share
  *                        one GPU (RCCL refuses two ranks on one device).
- * Collectives must be issued in the same order on every rank.  Ranks' window
- * plans must agree (equal shard sizes and the same zkmi_bases_precompute
- * choice); a mismatch is detected and reported as ZKMI_EINVAL on every rank. */
+ * Collectives must be issued in the same order on every rank.  Every sharded
+ * MSM is exactly one all-gather of one fixed size per rank (a status block and
+ * the bit sums), whatever each rank's shard, plan or local failure, so no rank
+ * can block in a collective its peers skip.  Ranks' window plans must agree
+ * (equal shard sizes and the same zkmi_bases_precompute / zkmi_msm_set_window
+ * choice); a mismatch, or a failure on any rank, is reported as ZKMI_EINVAL
+ * on every rank by zkmi_msm_wait.
+ * Streams: a process with a communicator uses the context stream, at most two
+ * MSM lanes (zkmi_msm_set_lanes is capped at 2 while a communicator exists)
+ * and the communicator's stream: 4 = GPU_MAX_HW_QUEUES, so the RCCL kernel,
+ * which waits for its peers, never shares a hardware queue with a lane's
+ * kernels.  Witness programs run on the context stream then. */
 typedef struct zkmi_comm zkmi_comm;
 #define ZKMI_COMM_ID_BYTES 128
 /* all-gather of `bytes` from every rank: recv = rank 0's bytes || rank 1's ... */

@@ -15,9 +15,11 @@
 //     GPU, as on a 1-GPU box: RCCL refuses two ranks on one device);
 //   * RCCL: when dev0 != dev1 (the unique id travels over the pipe).
 // Cases: plain and fixed-base-table shards, a ragged total, an empty shard,
-// window plans that differ between the ranks (must fail on both ranks), and
-// several MSMs in flight over one shard, whose plan is agreed once (host
-// transport: exactly one all-gather per MSM after the first).
+// window plans that differ between the ranks (a table on one rank only, or a
+// window pinned on one rank only, with MSMs of an agreed plan before it: must
+// fail on both ranks, never hang), several MSMs in flight over one shard
+// (host transport: exactly one all-gather per MSM), local-check failures and
+// an injected failure.
 #include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -158,9 +160,9 @@ int run_rank(int rank, int dev, Link link, bool use_rccl) {
     CHECK(memcmp(got, want, sizeof(got)) == 0, "sharded != global MSM (total %zu, table %d)", k.total, (int)k.table);
     if (rank == 0) printf("case total=%zu table=%d: %s\n", k.total, (int)k.table, memcmp(got, want, 64) ? "MISMATCH" : "ok");
   }
-  // one shard, several MSMs in flight: the window plan is agreed by the first
-  // submit only (later submits run no control collective); pinning another
-  // window on both ranks agrees a new plan
+  // one shard, several MSMs in flight: every sharded MSM is exactly one
+  // exchange (no plan-agreement collective); pinning another window on both
+  // ranks changes the plan everywhere
   {
     const size_t total = (1u << 17) + 5;
     size_t first = 0, count = 0;
@@ -173,7 +175,7 @@ int run_rank(int rank, int dev, Link link, bool use_rccl) {
           "inputs");
     uint64_t want[8] = {0};
     CHECK(full_msm(ctx, 21, 22, total, want), "full MSM");
-    for (int win : {0, 13}) {
+    for (int win : {0, 15}) {
       CHECK(zkmi_msm_set_window(ctx, win) == 0, "set window %d", win);
       const int calls0 = link_calls;
       zkmi_msm_job* jobs[3] = {nullptr, nullptr, nullptr};
@@ -181,15 +183,31 @@ int run_rank(int rank, int dev, Link link, bool use_rccl) {
       for (auto& j : jobs) {
         uint64_t got[8] = {0};
         CHECK(j && zkmi_msm_wait(j, got) == 0 && memcmp(got, want, sizeof(got)) == 0,
-              "cached-plan sharded MSM (window %d) != global", win);
+              "pipelined sharded MSM (window %d) != global", win);
       }
-      if (!use_rccl)  // one header exchange + three bit-sum exchanges
-        CHECK(link_calls - calls0 == 4, "window %d: %d host all-gathers for 3 MSMs", win, link_calls - calls0);
+      if (!use_rccl)  // three exchanges, nothing else
+        CHECK(link_calls - calls0 == 3, "window %d: %d host all-gathers for 3 MSMs", win, link_calls - calls0);
+    }
+    // the window changes on rank 1 only, after MSMs of one plan ran: both
+    // ranks fail (no rank waits in a collective the other skipped), and the
+    // communicator stays in step
+    CHECK(zkmi_msm_set_window(ctx, rank == 1 ? 11 : 0) == 0, "set window");  // auto = 13 at this shard size
+    {
+      zkmi_msm_job* j = nullptr;
+      uint64_t got[8] = {0};
+      int rc = zkmi_msm_sharded_submit(comm, b, 0, d, count, &j);
+      if (rc == 0) rc = zkmi_msm_wait(j, got);
+      CHECK(rc == ZKMI_EINVAL, "window changed on rank 1 only: rank %d returned %d", rank, rc);
     }
     CHECK(zkmi_msm_set_window(ctx, 0) == 0, "set window 0");
+    {
+      uint64_t got[8] = {0};
+      CHECK(zkmi_msm_sharded(comm, b, 0, d, count, got) == 0 && memcmp(got, want, sizeof(got)) == 0,
+            "sharded MSM after the one-rank window change != global");
+    }
     zkmi_dev_free(ctx, d);
     zkmi_bases_destroy(b);
-    if (rank == 0) printf("cached plan: ok\n");
+    if (rank == 0) printf("pipelined + one-rank window change: ok\n");
   }
   // different window plans on the two ranks must fail on BOTH ranks
   {

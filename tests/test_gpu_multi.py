@@ -175,3 +175,50 @@ def test_config5_2pow26_eight_shards_native_exchange(ctx):
     assert not errors, errors
     for r in range(nr):
         assert np.array_equal(results[r], want), r
+
+
+def test_stream_budget_with_communicator():
+    """Stream budget: while a communicator exists a context
+    holds at most GPU_MAX_HW_QUEUES = 4 streams -- the context stream, <= 2
+    MSM lanes and the communicator's -- so the RCCL kernel (which waits for
+    its peers) never shares a hardware queue with MSM work: lanes made before
+    the communicator beyond two are released, set_lanes is capped, and witness
+    programs run on the context stream.  Results are unchanged."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_l2_wprog import SHAPES, _batch
+    from zelana_amd import gpu, host_prover as H, wprog as W
+    c = gpu.Context(0)
+    try:
+        n = 1 << 15
+        b = c.bases_generate(seed=5, n=n)
+        s = c.scalars_generate(seed=6, n=n)
+        c.set_lanes(3)
+        assert c.lanes() == 3
+        jobs = [c.msm_submit(b, s, n) for _ in range(3)]  # one per lane: three lane streams
+        want = [c.msm_wait(j) for j in jobs][0]
+        assert c.stream_count() == 4  # context + 3 lanes
+        comm = gpu.Comm.rccl(c, gpu.comm_unique_id(), 1, 0)
+        assert c.lanes() == 2 and c.stream_count() == 4  # context + 2 lanes + communicator
+        c.set_lanes(3)
+        assert c.lanes() == 2
+        jobs = [comm.msm_submit(b, s, n) for _ in range(4)]
+        for j in jobs:
+            assert np.array_equal(c.msm_wait(j), want)
+        bal, tr, wd = SHAPES[0]
+        inp, w = _batch(5, bal, tr, wd)
+        _, _, plan = H.l2_record(inp, w)
+        _, zh = H.native_l2_block_circuit(inp, w)
+        wp = W.WitnessProgram(c, plan)
+        dz = gpu.DeviceBuffer(c, plan.num_vars * 32)
+        wp.run(H.l2_witness_inputs(inp, w), dz)
+        zg = np.zeros_like(zh)
+        dz.download(zg)
+        assert np.array_equal(zg, zh)
+        assert c.stream_count() == 4, c.stream_count()  # the program ran on the context stream
+        wp.close()
+        dz.free()
+        comm.close()
+        assert c.stream_count() == 3
+    finally:
+        c.close()

@@ -76,6 +76,8 @@ SIGNATURES = [
     ("zkmi_msm_wait", ctypes.c_int, [vp, u64p]),
     ("zkmi_msm_set_window", ctypes.c_int, [vp, ctypes.c_int]),
     ("zkmi_msm_set_lanes", ctypes.c_int, [vp, ctypes.c_int]),
+    ("zkmi_msm_get_lanes", ctypes.c_int, [vp]),
+    ("zkmi_ctx_stream_count", ctypes.c_int, [vp]),
     ("zkmi_msm_submit_shared", ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_int, sz, vp, sz, ctypes.POINTER(vp)]),
     ("zkmi_comm_unique_id", ctypes.c_int, [u8p]),
     ("zkmi_comm_init", ctypes.c_int, [vp, u8p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]),

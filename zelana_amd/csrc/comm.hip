@@ -51,37 +51,24 @@ int comm_allgather_device(zkmi_comm* c, hipStream_t lane_st, const void* d_send,
 }
 
 int comm_allgather_host(zkmi_comm* c, const void* send, void* recv, size_t bytes) {
-  if (c->kind == ZKMI_COMM_HOST) {
-    int rc = c->fn(c->user, send, recv, bytes);
-    if (rc) {
-      set_error("host all-gather callback failed (%d)", rc);
-      return ZKMI_EINVAL;
-    }
-    return 0;
+  if (c->kind != ZKMI_COMM_HOST) {
+    set_error("comm_allgather_host: RCCL communicator (its exchanges run on the device)");
+    return ZKMI_EINVAL;
   }
-  const size_t need = bytes * (size_t)(c->nranks + 1);
-  if (c->stage_bytes < need) {
-    if (c->d_stage) (void)hipFree(c->d_stage);
-    c->d_stage = nullptr;
-    c->stage_bytes = 0;
-    ZK_HIP(hipMalloc((void**)&c->d_stage, need));
-    c->stage_bytes = need;
+  int rc = c->fn(c->user, send, recv, bytes);
+  if (rc) {
+    set_error("host all-gather callback failed (%d)", rc);
+    return ZKMI_EINVAL;
   }
-  // on the control communicator: the data communicator's stream may hold
-  // bit-sum exchanges still waiting for their lanes, and a synchronous header
-  // exchange queued behind them would stall the MSM pipeline
-  uint8_t* d = (uint8_t*)c->d_stage;
-  ZK_HIP(hipMemcpyAsync(d, send, bytes, hipMemcpyHostToDevice, c->st_ctl));
-  ZK_NCCL(ncclAllGather(d, d + bytes, bytes, ncclUint8, (ncclComm_t)c->nccl_ctl, c->st_ctl));
-  ZK_HIP(hipMemcpyAsync(recv, d + bytes, bytes * c->nranks, hipMemcpyDeviceToHost, c->st_ctl));
-  ZK_HIP(hipStreamSynchronize(c->st_ctl));
   return 0;
 }
 
+// A failed rank's payload: zeros with the failure flag (word 0 of the status
+// block) set, in the same one exchange its peers run.
 int comm_fail_exchange(zkmi_comm* c, size_t words) {
   if (c->kind == ZKMI_COMM_HOST) {
     std::vector<uint32_t> me(words, 0), all(words * (size_t)c->nranks);
-    me[words - SHARD_STATUS_WORDS] = 1;
+    me[0] = 1;
     return c->fn(c->user, me.data(), all.data(), words * 4) ? ZKMI_EINVAL : 0;
   }
   const size_t need = words * (size_t)c->nranks;
@@ -98,7 +85,7 @@ int comm_fail_exchange(zkmi_comm* c, size_t words) {
   uint32_t* mine = c->d_fail + words * (size_t)c->rank;
   const uint32_t one = 1;
   ZK_HIP(hipMemsetAsync(mine, 0, words * 4, c->st));
-  ZK_HIP(hipMemcpyAsync(mine + words - SHARD_STATUS_WORDS, &one, 4, hipMemcpyHostToDevice, c->st));
+  ZK_HIP(hipMemcpyAsync(mine, &one, 4, hipMemcpyHostToDevice, c->st));
   ZK_NCCL(ncclAllGather(mine, c->d_fail, words * 4, ncclUint8, (ncclComm_t)c->nccl, c->st));
   ZK_HIP(hipStreamSynchronize(c->st));
   return 0;
@@ -116,14 +103,39 @@ static int comm_new(zkmi_ctx* ctx, int nranks, int rank, int kind, zkmi_comm** o
   c->nranks = nranks;
   c->rank = rank;
   c->kind = kind;
-  if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->st_ctl, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
+  // counted from here on; zkmi_comm_destroy uncounts a communicator with a stream
+  if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) == hipSuccess) {
+    ctx->nstreams++;
+    ctx->ncomm++;
+  } else {
+    c->st = nullptr;
+  }
+  if (!c->st || hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming) != hipSuccess) {
     (void)hipGetLastError();
     zkmi_comm_destroy(c);
     set_error("zkmi_comm_init: cannot create the communicator's stream / events");
     return ZKMI_EHIP;
+  }
+  // Stream budget: beside a communicator the context keeps at most
+  // MAX_LANES_WITH_COMM lanes; lanes created before it beyond that go (after
+  // their work), so context + lanes + this stream <= GPU_MAX_HW_QUEUES.
+  if (ctx->msm_lanes > MAX_LANES_WITH_COMM) ctx->msm_lanes = MAX_LANES_WITH_COMM;
+  if ((int)ctx->lanes.size() > MAX_LANES_WITH_COMM) {
+    (void)ctx_sync_all(ctx);
+    while ((int)ctx->lanes.size() > MAX_LANES_WITH_COMM) {
+      MsmLane* l = ctx->lanes.back();
+      ctx->lanes.pop_back();
+      if (ctx->acc_last == l) ctx->acc_last = nullptr;
+      l->ws.release_all();
+      (void)hipEventDestroy(l->fork);
+      (void)hipEventDestroy(l->consumed);
+      (void)hipEventDestroy(l->acc_done);
+      (void)hipStreamDestroy(l->st);
+      delete l;
+      ctx->nstreams--;
+    }
+    ctx->lane_next = 0;
   }
   *out = c;
   return 0;
@@ -166,17 +178,9 @@ int zkmi_comm_init(zkmi_ctx* ctx, const uint8_t id[ZKMI_COMM_ID_BYTES], int nran
     return ZKMI_EHIP;
   }
   c->nccl = nc;
-  ncclComm_t ctl = nullptr;
-  r = ncclCommSplit(nc, 0, rank, &ctl, nullptr);
-  if (r != ncclSuccess) {
-    set_error("ncclCommSplit (control communicator): %s", ncclGetErrorString(r));
-    zkmi_comm_destroy(c);
-    return ZKMI_EHIP;
-  }
-  c->nccl_ctl = ctl;
-  // failure-exchange buffer: 64K words per rank covers every window plan's
-  // bit sums (<= ~24K words for G2)
-  c->fail_words = (size_t)65536 * nranks;
+  // failure-exchange buffer: one sharded payload per rank (msm.hip
+  // SHARD_PAYLOAD_WORDS = 36,864 words)
+  c->fail_words = (size_t)36864 * nranks;
   if (hipMalloc((void**)&c->d_fail, c->fail_words * 4) != hipSuccess) {
     (void)hipGetLastError();
     set_error("zkmi_comm_init: cannot allocate the failure-exchange buffer");
@@ -205,16 +209,16 @@ int zkmi_comm_init_host(zkmi_ctx* ctx, int nranks, int rank, zkmi_allgather_fn a
 void zkmi_comm_destroy(zkmi_comm* c) {
   if (!c) return;
   ZK_DEVICE_GUARD(c->ctx);
-  if (c->st) (void)hipStreamSynchronize(c->st);
-  if (c->st_ctl) (void)hipStreamSynchronize(c->st_ctl);
-  if (c->nccl_ctl) ncclCommDestroy((ncclComm_t)c->nccl_ctl);
+  if (c->st) {
+    (void)hipStreamSynchronize(c->st);
+    c->ctx->nstreams--;
+    c->ctx->ncomm--;
+  }
   if (c->nccl) ncclCommDestroy((ncclComm_t)c->nccl);
-  if (c->d_stage) (void)hipFree(c->d_stage);
   if (c->d_fail) (void)hipFree(c->d_fail);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
   if (c->ev_out) (void)hipEventDestroy(c->ev_out);
   if (c->st) (void)hipStreamDestroy(c->st);
-  if (c->st_ctl) (void)hipStreamDestroy(c->st_ctl);
   delete c;
 }
 

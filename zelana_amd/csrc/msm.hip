@@ -423,55 +423,6 @@ __device__ __forceinline__ void rs_scalar_keys(const uint32_t* __restrict__ scal
   }
 }
 
-template <int C, bool BAL>
-__global__ void __launch_bounds__(RS_THREADS) k_rs_p1f_count(const uint32_t* __restrict__ scalars, size_t n, int Wp,
-                                                             uint32_t B, uint32_t NH, uint32_t lob, uint32_t CS,
-                                                             uint32_t nc1, uint32_t* __restrict__ cnt1) {
-  ZK_TAIL_WAVE();
-  extern __shared__ uint32_t hist[];
-  constexpr int W = msm_windows(C);
-  for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) hist[x] = 0;
-  __syncthreads();
-  const size_t base = (size_t)blockIdx.x * CS;
-  for (uint32_t k = threadIdx.x; k < CS && base + k < n; k += RS_THREADS) {
-    uint32_t key[W], val[W];
-    bool ok[W];
-    rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok);
-#pragma unroll
-    for (int w = 0; w < W; w++)
-      if (ok[w]) atomicAdd(&hist[key[w] >> lob], 1u);
-  }
-  __syncthreads();
-  for (uint32_t x = threadIdx.x; x < NH; x += RS_THREADS) cnt1[(size_t)x * nc1 + blockIdx.x] = hist[x];
-}
-
-// T threads: a sub-tile is T scalars (T * W entries); 1024 gives 4x longer
-// runs per bin than 256 (one workgroup per CU, 16 waves)
-template <int C, int T, bool BAL>
-__global__ void __launch_bounds__(T) k_rs_p1f_scatter(const uint32_t* __restrict__ scalars, size_t n, int Wp,
-                                                               uint32_t B, uint32_t NH, uint32_t lob, uint32_t CS,
-                                                               uint32_t nc1, const uint32_t* __restrict__ offs1,
-                                                               uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
-  ZK_TAIL_WAVE();
-  extern __shared__ uint32_t lds[];
-  constexpr int W = msm_windows(C);
-  for (uint32_t x = threadIdx.x; x < NH; x += T) lds[2 * NH + x] = offs1[(size_t)x * nc1 + blockIdx.x];
-  const size_t base = (size_t)blockIdx.x * CS;
-  const uint32_t cnt = (uint32_t)std::min<size_t>(CS, n - base);
-  auto fill = [&](uint32_t sub, uint32_t* key, uint32_t* val, bool* ok) {
-    const uint32_t k = sub * T + threadIdx.x;
-    if (k < cnt) {
-      rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok);
-    } else {
-#pragma unroll
-      for (int w = 0; w < W; w++) ok[w] = false;
-    }
-  };
-  auto bin = [lob](uint32_t key) { return key >> lob; };
-  rs_scatter_core<W, decltype(fill), decltype(bin), true, T>((cnt + T - 1) / T, NH, lds, fill, bin,
-                                                          okey, oval);
-}
-
 // Small sorts (<= SMALL_SORT_MAX entries: the small proofs' MSMs, ~10^5
 // entries over a few thousand buckets) are latency-bound: the two-pass radix
 // sort's ~11 launches cost ~180 us per MSM there.  Counting sort with global
@@ -668,6 +619,319 @@ __global__ void __launch_bounds__(256) k_rs_bstart(const uint32_t* __restrict__ 
   }
   uint32_t h = k >> lob, lo = k & ((1u << lob) - 1), nt = tstart[h + 1] - tstart[h];
   bstart[k] = nt ? offs2[((size_t)tstart[h] << lob) + (size_t)lo * nt] : binstart[h];
+}
+
+// ------------------------------------------------------------- bin sort
+// The sort of every MSM with windows c >= 12 (fused digits): four kernels,
+// no device-wide scan, every workgroup 256 threads (one wave per SIMD, so it
+// fits beside the accumulation waves of another lane):
+//   A k_bs_count    chunk of CS scalars -> LDS histogram of the hi bins (key
+//                   >> lob); per (chunk, bin) one atomicAdd on the bin total
+//                   and one returning atomicAdd on the (super-chunk, bin)
+//                   total, which IS the chunk's offset inside that super-chunk
+//                   of the bin (a super-chunk = 1/32 of the scalars).
+//   B k_bs_scatter1 the chunk's entries into their bins at binstart (block
+//                   prefix of the bin totals) + the earlier super-chunks of
+//                   the bin + that offset, LDS-staged runs (rs_scatter_core).
+//   C k_bs_count2   tiles of <= C2 entries inside one bin -> LDS histogram of
+//                   the lo keys, stored per tile.
+//   D k_bs_scatter2 each tile sums its bin's tile histograms (bucket sizes,
+//                   and its own offset inside every bucket: the earlier tiles'
+//                   counts), prefixes the sizes (bucket starts), scatters;
+//                   tile 0 of a bin writes the bin's bstart and, for
+//                   one-lane-per-bucket plans, the bin's accumulation items.
+// Entries of a bucket therefore stay in scalar order up to 1/32 of the range
+// (random only inside a super-chunk).  That order is what the accumulation
+// gathers by: at step p every lane of a wave (equal bucket lengths) reads a
+// table row of about the same scalar index, so the wave's 64 gathers share a
+// few pages per table copy.  (Measured, round 5: with chunk offsets in atomic
+// arrival order -- random inside every bucket -- the 2^20 accumulation issued
+// 2.6% more VALU instructions but ran 25% longer, 1045 vs 867 us one lane;
+// VALU issue 0.75 vs 0.91.)
+// Counters: one memset of the bin / super-chunk totals and item counters at
+// the sort's start.
+// (Replaces the two-pass radix sort's three-launch scans, its tiles / bstart
+// kernels and the four-launch item plan: in the r04 3-lane trace the P2 scan
+// of a 3.9M-entry [bin][lo][tile] count matrix alone sat ~150 us on the
+// critical path between two accumulations.)
+constexpr uint32_t BS_NSC = 32;  // super-chunks
+
+// exclusive prefix, in index order, of get(0..nb) into out[0..nb) (LDS) by T
+// threads; returns the total.  tmp: T/64 words of LDS.  Ends with a barrier.
+template <int T, class Get>
+__device__ __forceinline__ uint32_t block_prefix(uint32_t nb, Get get, uint32_t* out, uint32_t* tmp) {
+  const uint32_t per = (nb + T - 1) / T, k0 = min(nb, threadIdx.x * per), k1 = min(nb, k0 + per);
+  uint32_t sum = 0;
+  for (uint32_t k = k0; k < k1; k++) sum += get(k);
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= (unsigned)off) inc += t;
+  }
+  if (lane == 63) tmp[wid] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum, total = 0;
+#pragma unroll
+  for (int w = 0; w < T / 64; w++) {
+    const uint32_t tw = tmp[w];
+    if ((uint32_t)w < wid) run += tw;
+    total += tw;
+  }
+  for (uint32_t k = k0; k < k1; k++) {
+    const uint32_t v = get(k);
+    out[k] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+template <int C, bool BAL>
+__global__ void __launch_bounds__(256) k_bs_count(const uint32_t* __restrict__ scalars, size_t n, int Wp, uint32_t B,
+                                                  uint32_t NH, uint32_t lob, uint32_t CS, uint32_t scs,
+                                                  uint32_t* __restrict__ bintot, uint32_t* __restrict__ sctot,
+                                                  uint32_t* __restrict__ choff, uint32_t* __restrict__ next_ctr,
+                                                  uint32_t ctr_words) {
+  ZK_TAIL_WAVE();
+  extern __shared__ uint32_t hist[];
+  constexpr int W = msm_windows(C);
+  // the lane's other counter block, for its next sort
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < ctr_words; i += (size_t)gridDim.x * 256) next_ctr[i] = 0;
+  for (uint32_t x = threadIdx.x; x < NH; x += 256) hist[x] = 0;
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * CS;
+  for (uint32_t k = threadIdx.x; k < CS && base + k < n; k += 256) {
+    uint32_t key[W], val[W];
+    bool ok[W];
+    rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok);
+#pragma unroll
+    for (int w = 0; w < W; w++)
+      if (ok[w]) atomicAdd(&hist[key[w] >> lob], 1u);
+  }
+  __syncthreads();
+  uint32_t* sc = sctot + (size_t)(blockIdx.x >> scs) * NH;
+  for (uint32_t x = threadIdx.x; x < NH; x += 256) {
+    const uint32_t hx = hist[x];
+    uint32_t off = 0;
+    if (hx) {
+      off = atomicAdd(&sc[x], hx);
+      atomicAdd(&bintot[x], hx);
+    }
+    choff[(size_t)blockIdx.x * NH + x] = off;
+  }
+}
+
+// T threads, sub-tiles of T scalars (T * W entries)
+template <int C, int T, bool BAL>
+__global__ void __launch_bounds__(T) k_bs_scatter1(const uint32_t* __restrict__ scalars, size_t n, int Wp, uint32_t B,
+                                                   uint32_t NH, uint32_t lob, uint32_t CS, uint32_t scs,
+                                                   const uint32_t* __restrict__ bintot,
+                                                   const uint32_t* __restrict__ sctot,
+                                                   const uint32_t* __restrict__ choff, uint32_t* __restrict__ okey,
+                                                   uint32_t* __restrict__ oval) {
+  ZK_TAIL_WAVE();
+  extern __shared__ uint32_t lds[];
+  constexpr int W = msm_windows(C);
+  uint32_t* gbase = lds + 2 * NH;
+  block_prefix<T>(NH, [&](uint32_t k) { return bintot[k]; }, gbase, lds + 3 * NH);
+  const uint32_t s0 = blockIdx.x >> scs;  // this chunk's super-chunk: the earlier ones come first in every bin
+  for (uint32_t x = threadIdx.x; x < NH; x += T) {
+    uint32_t g = gbase[x] + choff[(size_t)blockIdx.x * NH + x];
+    for (uint32_t q = 0; q < s0; q++) g += sctot[(size_t)q * NH + x];
+    gbase[x] = g;
+  }
+  const size_t base = (size_t)blockIdx.x * CS;
+  const uint32_t cnt = (uint32_t)std::min<size_t>(CS, n - base);
+  auto fill = [&](uint32_t sub, uint32_t* key, uint32_t* val, bool* ok) {
+    const uint32_t k = sub * T + threadIdx.x;
+    if (k < cnt) {
+      rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok);
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; w++) ok[w] = false;
+    }
+  };
+  auto bin = [lob](uint32_t key) { return key >> lob; };
+  rs_scatter_core<W, decltype(fill), decltype(bin), true, T>((cnt + T - 1) / T, NH, lds, fill, bin, okey, oval);
+}
+
+// Tile geometry of C / D, recomputed by every workgroup from the bin totals:
+// pre[0..NH] bin starts, tst[0..NH] tile starts (every bin has >= 1 tile, so
+// tile 0 of every bin exists to write its bstart).  Returns the total tiles.
+__device__ __forceinline__ uint32_t bs_tiles(const uint32_t* __restrict__ bintot, uint32_t NH, uint32_t C2,
+                                             uint32_t* pre, uint32_t* tst, uint32_t* tmp) {
+  const uint32_t M = block_prefix<256>(NH, [&](uint32_t k) { return bintot[k]; }, pre, tmp);
+  const uint32_t TT = block_prefix<256>(
+      NH, [&](uint32_t k) { return max(1u, (bintot[k] + C2 - 1) / C2); }, tst, tmp);
+  if (threadIdx.x == 0) {
+    pre[NH] = M;
+    tst[NH] = TT;
+  }
+  __syncthreads();
+  return TT;
+}
+
+__global__ void __launch_bounds__(256) k_bs_count2(const uint32_t* __restrict__ okey,
+                                                   const uint32_t* __restrict__ bintot, uint32_t NH, uint32_t lob,
+                                                   uint32_t C2, uint32_t T2max, uint32_t* __restrict__ thist) {
+  ZK_TAIL_WAVE();
+  extern __shared__ uint32_t lds[];
+  const uint32_t NLO = 1u << lob, mask = NLO - 1;
+  uint32_t* hist = lds;
+  uint32_t* pre = lds + NLO;
+  uint32_t* tst = pre + NH + 1;
+  uint32_t* tmp = tst + NH + 1;
+  const uint32_t t = rs_xcd_tile(blockIdx.x, T2max);
+  if (t >= T2max) return;  // beyond any tile count (block-uniform)
+  const uint32_t TT = bs_tiles(bintot, NH, C2, pre, tst, tmp);
+  if (t >= TT) return;
+  const uint32_t h = rs_tile_bin(tst, NH, t), q = t - tst[h];
+  const uint32_t lo = pre[h] + q * C2, hi = min(lo + C2, pre[h + 1]);
+  for (uint32_t x = threadIdx.x; x < NLO; x += 256) hist[x] = 0;
+  __syncthreads();
+  constexpr int U = 8;  // loads in flight per thread
+  for (uint32_t p0 = lo; p0 < hi; p0 += U * 256) {
+    uint32_t kk[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t p = p0 + u * 256 + threadIdx.x;
+      kk[u] = p < hi ? okey[p] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (kk[u] != 0xFFFFFFFFu) atomicAdd(&hist[kk[u] & mask], 1u);
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < NLO; x += 256) thist[(size_t)t * NLO + x] = hist[x];
+}
+
+// Accumulation items of one-lane-per-bucket plans (k_acc_items_*): tile 0 of
+// every bin ranks the bin's buckets by length (pieces capped at `cap`),
+// longest first, stages them per bin and adds the bin's class counts to the
+// global class histogram; k_items_place then lays the items out class-major
+// over all bins (each bin's run of a class contiguous), as round 4's item plan
+// did.  Waves then hold buckets of one length, and the items run longest
+// first.  That global class order is what the accumulation's speed rests on:
+// measured (round 5, one lane, the same sort), the accumulation took 906 us
+// with it, 1086 us with the items ranked inside each bin and the bins
+// interleaved wave by wave (ranks 64r..64r+63 of bin h per wave), and ~1045-
+// 1150 us with one rank of 64 bins per wave -- waves of one class run their
+// gathers in step.  A bucket longer than cap keeps its first piece in place;
+// pieces 1.. go to the overflow items after the nmain main slots (run first),
+// and the bucket to the split list the piece sums read.  A bucket longer than cap keeps its first
+// piece in place; pieces 1.. go to the overflow items after the nmain main
+// slots (run first), and the bucket to the split list the piece sums read.
+// itc: [0] overflow items, [1] partial slots, [2] split buckets.
+struct ItemsOut {
+  uint4* items;
+  uint32_t nmain, cap;
+  uint32_t* itc;
+  uint4* split;
+  uint4* stage;     // [NH][NLO]: a bin's items by class, longest first (k_items_place reads them)
+  uint32_t* ghist;  // [cap + 1]: buckets per class over all bins
+};
+
+template <int ST, bool ITEMS>
+__global__ void __launch_bounds__(256) k_bs_scatter2(const uint32_t* __restrict__ okey,
+                                                     const uint32_t* __restrict__ oval,
+                                                     const uint32_t* __restrict__ bintot, uint32_t NH, uint32_t lob,
+                                                     uint32_t C2, uint32_t T2max, uint32_t K,
+                                                     const uint32_t* __restrict__ thist,
+                                                     uint32_t* __restrict__ sval, uint32_t* __restrict__ bstart,
+                                                     ItemsOut io) {
+  ZK_TAIL_WAVE();
+  constexpr int T = 256;
+  extern __shared__ uint32_t lds[];
+  const uint32_t NLO = 1u << lob, mask = NLO - 1;
+  // rs_scatter_core layout first, then the tile geometry
+  uint32_t* lstart = lds + NLO;
+  uint32_t* gbase = lds + 2 * NLO;
+  uint32_t* tmp = lds + 3 * NLO;
+  uint32_t* skey = tmp + T;
+  uint32_t* pre = skey + 2 * ST;
+  uint32_t* tst = pre + NH + 1;
+  const uint32_t t = rs_xcd_tile(blockIdx.x, T2max);
+  if (t >= T2max) return;
+  const uint32_t TT = bs_tiles(bintot, NH, C2, pre, tst, tmp);
+  if (t >= TT) return;
+  const uint32_t h = rs_tile_bin(tst, NH, t), q = t - tst[h];
+  const uint32_t lo = pre[h] + q * C2, hi = min(lo + C2, pre[h + 1]);
+  const uint32_t k0 = h * NLO;  // first key of the bin
+  // bucket sizes (all tiles of the bin) and this tile's offset inside every
+  // bucket (the earlier tiles' counts: entries keep the bin's order)
+  uint32_t* ksz = lds;  // the scatter's hist array, free until rs_scatter_core
+  {
+    const uint32_t t0 = tst[h], nt = tst[h + 1] - t0;
+    for (uint32_t x = threadIdx.x; x < NLO; x += T) {
+      uint32_t tot = 0, before = 0;
+      for (uint32_t qq = 0; qq < nt; qq++) {
+        const uint32_t v = thist[(size_t)(t0 + qq) * NLO + x];
+        before += qq < q ? v : 0u;
+        tot += v;
+      }
+      ksz[x] = k0 + x < K ? tot : 0u;
+      gbase[x] = before;
+    }
+    __syncthreads();
+  }
+  auto ksize = [&](uint32_t x) { return ksz[x]; };
+  // bucket starts inside the bin
+  block_prefix<T>(NLO, ksize, lstart, tmp);
+  if (q == 0) {
+    for (uint32_t x = threadIdx.x; x < NLO; x += T)
+      if (k0 + x < K) bstart[k0 + x] = pre[h] + lstart[x];
+    if (h == NH - 1 && threadIdx.x == 0) bstart[K] = pre[NH];
+    if constexpr (ITEMS) {
+      // rank the bin's buckets by capped length, longest first (LDS counting
+      // sort over the classes 0..cap)
+      const uint32_t cap = io.cap;
+      uint32_t* ch = skey;         // class histogram [cap + 1]
+      uint32_t* cstart = skey + ST;  // descending class starts [cap + 1]
+      for (uint32_t c = threadIdx.x; c <= cap; c += T) ch[c] = 0;
+      __syncthreads();
+      constexpr uint32_t PERX = 2048 / T;  // NLO <= 2048
+      uint32_t tk[PERX];
+#pragma unroll
+      for (uint32_t j = 0; j < PERX; j++) {
+        const uint32_t x = j * T + threadIdx.x;
+        if (x < NLO) tk[j] = atomicAdd(&ch[min(ksize(x), cap)], 1u);
+      }
+      __syncthreads();
+      block_prefix<T>(cap + 1, [&](uint32_t k) { return ch[cap - k]; }, cstart, tmp);
+#pragma unroll
+      for (uint32_t j = 0; j < PERX; j++) {
+        const uint32_t x = j * T + threadIdx.x;
+        if (x >= NLO) continue;
+        const uint32_t size = ksize(x), cls = min(size, cap);
+        const uint32_t rank = cstart[cap - cls] + tk[j];
+        const uint32_t start = pre[h] + lstart[x];
+        const uint32_t np = (size + cap - 1) / cap;
+        uint32_t slot0 = 0xFFFFFFFFu;  // NOSLOT: no partial slot
+        if (np > 1) {
+          slot0 = atomicAdd(&io.itc[1], np);
+          const uint32_t ov = atomicAdd(&io.itc[0], np - 1);
+          io.split[atomicAdd(&io.itc[2], 1u)] = make_uint4(k0 + x, slot0, np, 0);
+          for (uint32_t pc = 1; pc < np; pc++)
+            io.items[io.nmain + ov + pc - 1] =
+                make_uint4(start + pc * cap, min(start + (pc + 1) * cap, start + size), k0 + x, slot0 + pc);
+        }
+        io.stage[(size_t)h * NLO + rank] = make_uint4(start, start + cls, k0 + x, slot0);
+      }
+      for (uint32_t c = threadIdx.x; c <= cap; c += T)
+        if (ch[c]) atomicAdd(&io.ghist[c], ch[c]);
+      __syncthreads();
+    }
+  }
+  for (uint32_t x = threadIdx.x; x < NLO; x += T) gbase[x] += pre[h] + lstart[x];
+  auto load = [&](uint32_t e, uint32_t& key, uint32_t& val) {
+    key = okey[lo + e];
+    val = oval[lo + e];
+    return true;
+  };
+  auto bin = [mask](uint32_t key) { return key & mask; };
+  rs_scatter_tiles<ST, decltype(load), decltype(bin), false, T>(hi - lo, NLO, lds, load, bin, nullptr, sval);
 }
 
 // ----------------------------------------------------------------- scan
@@ -1041,122 +1305,42 @@ struct Acc0Kernel<G2T> {
 // For >= 2^18 buckets (fixed-base tables with c >= 19) the accumulation gives
 // each lane a whole bucket: no chunk edges, so no partial sums (except for
 // buckets longer than `cap`, split into cap-sized pieces), and no bucket
-// boundaries inside a lane's loop.  Work items are ordered by length,
-// longest first: the 64 lanes of a wave get equal trip counts and the waves
-// that run last are the shortest, so the tail is short.  (The chunked path
-// loses ~15% to its tail: resident waves of a SIMD finish in age order, the
-// last one alone and latency-bound; tools/trace_acc0.py.)
+// boundaries inside a lane's loop.  The items (k_bs_scatter2) are ranked by
+// length inside each bin and interleaved over the bins: the 64 lanes of a
+// wave get about equal trip counts and the waves that run last are the
+// shortest, so the tail is short.  (The chunked path loses ~15% to its tail:
+// resident waves of a SIMD finish in age order, the last one alone and
+// latency-bound; tools/trace_acc0.py.)
 constexpr uint32_t ITEM_CAP_MAX = 1024;
 constexpr uint32_t ITEMS_MIN_K = 1u << 18;
-constexpr uint32_t ITEM_SEQ_MAX = 32;  // pieces summed by one thread (k_items_combine)
 constexpr uint32_t NOSLOT = 0xFFFFFFFFu;
 
-// ITEMS_IPT buckets per thread (strided by 256): a workgroup then covers 2K
-// buckets, so the per-class global atomics at its end (bucket sizes of a
-// uniform MSM fall into ~20 classes) see 256 workgroups for 2^19 buckets
-// rather than 2048 -- same-address atomics serialise in L2.
-constexpr uint32_t ITEMS_IPT = 8;
-__global__ void __launch_bounds__(256) k_items_count(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
-                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ hv,
-                                                     uint32_t* __restrict__ open_flag) {
-  ZK_TAIL_WAVE();
-  __shared__ uint32_t lh[ITEM_CAP_MAX + 1];
-  for (uint32_t i = threadIdx.x; i <= cap; i += 256) lh[i] = 0;
-  __syncthreads();
-  bool open = false;
-#pragma unroll
-  for (uint32_t q = 0; q < ITEMS_IPT; q++) {
-    const uint32_t b = (blockIdx.x * ITEMS_IPT + q) * 256 + threadIdx.x;
-    if (b < K) {
-      const uint32_t size = bstart[b + 1] - bstart[b];
-      const uint32_t np = (size + cap - 1) / cap;
-      if (size) {
-        if (np > 1) atomicAdd(&lh[cap], np - 1);
-        atomicAdd(&lh[size - (np - 1) * cap], 1u);
-      }
-      hv[b] = np > 1 ? np : 0;
-      open |= np > ITEM_SEQ_MAX;
-    }
+// item of lane i: the overflow pieces (full cap-length pieces of split
+// buckets) first, then the nmain main slots; empty slots (start == end) are
+// buckets without entries.  Returns false when the lane has nothing to add.
+__device__ __forceinline__ bool item_of(const uint4* __restrict__ items, uint32_t nover, uint32_t nmain, uint32_t i,
+                                        uint4& it) {
+  uint32_t idx;
+  if (i < nover) {  // (nover <= the grid's npieces by construction)
+    idx = nmain + i;
+  } else {
+    idx = i - nover;
+    if (idx >= nmain) return false;
   }
-  if (open) atomicOr(open_flag, 1u);
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i <= cap; i += 256)
-    if (lh[i]) atomicAdd(&hist[i], lh[i]);
-}
-
-// one thread: cursors of the size classes, longest class first; total items
-__global__ void k_items_offsets(const uint32_t* __restrict__ hist, uint32_t cap, uint32_t* __restrict__ cursor,
-                                uint32_t* __restrict__ nitems) {
-  ZK_TAIL_WAVE();
-  uint32_t run = 0;
-  for (uint32_t cl = cap; cl >= 1; cl--) {
-    cursor[cl] = run;
-    run += hist[cl];
-  }
-  nitems[0] = run;
-}
-
-// Also resets the partial list the segmented cascade reads (xkey = no key,
-// xvalid = 0) -- only when k_items_count found a bucket the cascade must
-// finish (open_flag); otherwise no cascade level reads the list.
-__global__ void __launch_bounds__(256) k_items_scatter(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
-                                                       const uint32_t* __restrict__ pbase,
-                                                       uint32_t* __restrict__ cursor, uint4* __restrict__ items,
-                                                       const uint32_t* __restrict__ open_flag, uint32_t* __restrict__ xkey,
-                                                       uint32_t* __restrict__ xvalid, uint32_t xl) {
-  ZK_TAIL_WAVE();
-  if (*open_flag) {
-    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < xl; i += (size_t)gridDim.x * 256) {
-      xkey[i] = 0xFFFFFFFFu;
-      xvalid[i] = 0;
-    }
-  }
-  __shared__ uint32_t lc[ITEM_CAP_MAX + 1], lbase[ITEM_CAP_MAX + 1];
-  for (uint32_t i = threadIdx.x; i <= cap; i += 256) lc[i] = 0;
-  __syncthreads();
-  uint32_t r_full[ITEMS_IPT], r_last[ITEMS_IPT];
-#pragma unroll
-  for (uint32_t q = 0; q < ITEMS_IPT; q++) {
-    const uint32_t b = (blockIdx.x * ITEMS_IPT + q) * 256 + threadIdx.x;
-    r_full[q] = r_last[q] = 0;
-    if (b < K) {
-      const uint32_t size = bstart[b + 1] - bstart[b];
-      const uint32_t np = (size + cap - 1) / cap;
-      if (size) {
-        if (np > 1) r_full[q] = atomicAdd(&lc[cap], np - 1);
-        r_last[q] = atomicAdd(&lc[size - (np - 1) * cap], 1u);
-      }
-    }
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i <= cap; i += 256) lbase[i] = lc[i] ? atomicAdd(&cursor[i], lc[i]) : 0;
-  __syncthreads();
-#pragma unroll
-  for (uint32_t q = 0; q < ITEMS_IPT; q++) {
-    const uint32_t b = (blockIdx.x * ITEMS_IPT + q) * 256 + threadIdx.x;
-    if (b >= K) continue;
-    const uint32_t lo = bstart[b], size = bstart[b + 1] - lo;
-    if (!size) continue;
-    const uint32_t np = (size + cap - 1) / cap, cl_last = size - (np - 1) * cap;
-    const uint32_t pb = np > 1 ? pbase[b] : NOSLOT;
-    for (uint32_t k = 0; k + 1 < np; k++)
-      items[lbase[cap] + r_full[q] + k] = make_uint4(lo + k * cap, lo + (k + 1) * cap, b, pb + k);
-    items[lbase[cl_last] + r_last[q]] = make_uint4(lo + (np - 1) * cap, lo + size, b, np > 1 ? pb + (np - 1) : NOSLOT);
-  }
+  it = items[idx];
+  return it.x != it.y;
 }
 
 template <class G>
-__device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
-                                               const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                                                                                              uint32_t tn, uint32_t tskip, uint32_t* __restrict__ buckets,
-                                               uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                                               uint32_t* __restrict__ xpts) {
+__device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, const uint32_t* __restrict__ nover,
+                                               uint32_t nmain, const uint32_t* __restrict__ sval,
+                                               const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
+                                               uint32_t* __restrict__ buckets, uint32_t* __restrict__ xpts) {
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   constexpr int PQ = G::PW / 4;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *nitems) return;
-  const uint4 it = items[i];
+  uint4 it;
+  if (!item_of(items, *nover, nmain, blockIdx.x * blockDim.x + threadIdx.x, it)) return;
   const uint32_t start = it.x, end = it.y;
   auto row = [&](uint32_t v) {
     uint32_t idx = v & 0x7FFFFFFFu;
@@ -1219,13 +1403,7 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
       else acc = xyzz_madd_g2(acc, P);
     }
   }
-  if (it.w == NOSLOT) {
-    st_acc<G>(buckets + (size_t)it.z * XW, acc);
-  } else {
-    xkey[it.w] = it.z;
-    xvalid[it.w] = 1;
-    st_acc<G>(xpts + (size_t)it.w * XW, acc);
-  }
+  st_acc<G>(it.w == NOSLOT ? buckets + (size_t)it.z * XW : xpts + (size_t)it.w * XW, acc);
 }
 // G1 one-lane-per-item accumulation (the dominant kernel of a table MSM):
 // rows gathered one entry ahead, the first finite point
@@ -1235,16 +1413,15 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
 // pass).  The rare
 // states (a base at infinity, the empty or one-point accumulator after a
 // cancellation) branch per lane; lanes of a wave have equal trip counts.
-__device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
-                                              const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                                              uint32_t tn, uint32_t tskip,
-                                              uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey,
-                                              uint32_t* __restrict__ xvalid, uint32_t* __restrict__ xpts,
+__device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, const uint32_t* __restrict__ nover,
+                                              uint32_t nmain, const uint32_t* __restrict__ sval,
+                                              const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
+                                              uint32_t* __restrict__ buckets, uint32_t* __restrict__ xpts,
                                               uint32_t i) {
   using F = FqOps;
   constexpr int XW = 32;
-  if (i >= *nitems) return;
-  const uint4 it = items[i];
+  uint4 it;
+  if (!item_of(items, *nover, nmain, i, it)) return;
   const uint32_t start = it.x, end = it.y;
   auto row = [&](uint32_t v) {
     uint32_t idx = v & 0x7FFFFFFFu;
@@ -1307,22 +1484,13 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
     step(cr, v);
   }
   if (phase == 0) acc = xyzz_inf<F>();
-  if (it.w == NOSLOT) {
-    st_acc<G1T>(buckets + (size_t)it.z * XW, acc);
-  } else {
-    xkey[it.w] = it.z;
-    xvalid[it.w] = 1;
-    st_acc<G1T>(xpts + (size_t)it.w * XW, acc);
-  }
+  st_acc<G1T>(it.w == NOSLOT ? buckets + (size_t)it.z * XW : xpts + (size_t)it.w * XW, acc);
 }
 __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
-    k_acc_items_g1(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
-                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                   uint32_t tn, uint32_t tskip,
-                   uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                   uint32_t* __restrict__ xpts) {
-  acc_items_g1f(items, nitems, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts,
-                     blockIdx.x * blockDim.x + threadIdx.x);
+    k_acc_items_g1(const uint4* __restrict__ items, const uint32_t* __restrict__ nover, uint32_t nmain,
+                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases, uint32_t tn,
+                   uint32_t tskip, uint32_t* __restrict__ buckets, uint32_t* __restrict__ xpts) {
+  acc_items_g1f(items, nover, nmain, sval, bases, tn, tskip, buckets, xpts, blockIdx.x * blockDim.x + threadIdx.x);
 }
 // (Tried for the 3-lane pipeline: rows staged through LDS by
 // global_load_lds, and a persistent form with one 768-thread workgroup per CU
@@ -1331,38 +1499,100 @@ __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
 // accumulation running) but the accumulation itself slowed by as much:
 // 2^20 3-lane 1.24-1.29 ms/step against 1.17-1.20; dropped.)
 __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK)
-    k_acc_items_g2(const uint4* __restrict__ items, const uint32_t* __restrict__ nitems,
-                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases,
-                   uint32_t tn, uint32_t tskip,
-                   uint32_t* __restrict__ buckets, uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                   uint32_t* __restrict__ xpts) {
-  acc_items_body<G2T>(items, nitems, sval, bases, tn, tskip, buckets, xkey, xvalid, xpts);
+    k_acc_items_g2(const uint4* __restrict__ items, const uint32_t* __restrict__ nover, uint32_t nmain,
+                   const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases, uint32_t tn,
+                   uint32_t tskip, uint32_t* __restrict__ buckets, uint32_t* __restrict__ xpts) {
+  acc_items_body<G2T>(items, nover, nmain, sval, bases, tn, tskip, buckets, xpts);
 }
 
-// Buckets split into 2..ITEM_SEQ_MAX pieces: one thread sums them (contiguous
-// partial slots) and invalidates them; longer ones stay for k_msm_accN.
+// Global class order of the items (one workgroup per bin): class starts from
+// the class histogram (longest class first), this bin's offset inside every
+// class by one returning atomicAdd per class, then the bin's staged items
+// (already class-ordered) copied to their slots.  Items are dense over
+// [0, NH * NLO): every bucket has one main item (class 0 = empty, run last).
+__global__ void __launch_bounds__(256) k_items_place(const uint4* __restrict__ stage, uint32_t NLO, uint32_t cap,
+                                                     const uint32_t* __restrict__ ghist, uint32_t* __restrict__ gcur,
+                                                     uint4* __restrict__ items, uint32_t nmain) {
+  ZK_TAIL_WAVE();
+  __shared__ uint32_t lh[ITEM_CAP_MAX + 1], lstart[ITEM_CAP_MAX + 1], base[ITEM_CAP_MAX + 1], tmp[4];
+  const uint32_t h = blockIdx.x;
+  const uint4* st = stage + (size_t)h * NLO;
+  for (uint32_t c = threadIdx.x; c <= cap; c += 256) lh[c] = 0;
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < NLO; x += 256) {
+    const uint4 it = st[x];
+    atomicAdd(&lh[min(it.y - it.x, cap)], 1u);
+  }
+  __syncthreads();
+  // the bin's class runs (descending) and the global class starts
+  block_prefix<256>(cap + 1, [&](uint32_t k) { return lh[cap - k]; }, lstart, tmp);
+  block_prefix<256>(cap + 1, [&](uint32_t k) { return ghist[cap - k]; }, base, tmp);
+  for (uint32_t k = threadIdx.x; k <= cap; k += 256) {
+    const uint32_t c = cap - k;
+    if (lh[c]) base[k] += atomicAdd(&gcur[c], lh[c]);
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < NLO; x += 256) {
+    const uint4 it = st[x];
+    const uint32_t k = cap - min(it.y - it.x, cap);
+    const uint32_t dst = base[k] + (x - lstart[k]);
+    if (dst < nmain) items[dst] = it;  // always (the class counts cover exactly nmain items)
+  }
+}
+
+// Piece sums of the split buckets (k_bs_scatter2's split list: key, first
+// partial slot, pieces): one wave per bucket, every lane folds its strided
+// share of the pieces, then a 6-level LDS tree -- ~log2(pieces) dependent
+// additions however heavy the bucket (a witness-like MSM's bucket of the
+// digit 1 holds a large share of the entries).  One curve-addition call site
+// in one block-uniform loop, as the bucket reduction.  A uniform MSM splits
+// nothing: the launch reads the count and exits.
 template <class G>
-__global__ void __launch_bounds__(256) k_items_combine(const uint32_t* __restrict__ bstart, uint32_t K, uint32_t cap,
-                                                       const uint32_t* __restrict__ pbase,
-                                                       uint32_t* __restrict__ buckets, uint32_t* __restrict__ xvalid,
+__global__ void __launch_bounds__(256) k_split_combine(const uint4* __restrict__ split,
+                                                       const uint32_t* __restrict__ nsplit,
                                                        const uint32_t* __restrict__ xpts,
-                                                       const uint32_t* __restrict__ npieces) {
+                                                       uint32_t* __restrict__ buckets) {
   ZK_TAIL_WAVE();
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= K || *npieces == 0) return;  // no bucket was split (uniform data: the usual case)
-  const uint32_t size = bstart[b + 1] - bstart[b];
-  const uint32_t np = (size + cap - 1) / cap;
-  if (np < 2 || np > ITEM_SEQ_MAX) return;
-  const uint32_t s0 = pbase[b];
-  Xyzz<F> sum = ld_xyzz<G>(xpts + (size_t)s0 * XW);
-  xvalid[s0] = 0;
-  for (uint32_t q = 1; q < np; q++) {
-    sum = br_add<G>(sum, ld_xyzz<G>(xpts + (size_t)(s0 + q) * XW));
-    xvalid[s0 + q] = 0;
+  __shared__ Xyzz<F> sh[4][32];
+  __shared__ uint32_t nl[4];
+  const uint32_t ns = *nsplit;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t base = blockIdx.x * 4; base < ns; base += gridDim.x * 4) {  // block-uniform
+    const uint32_t j = base + wave;
+    const bool live = j < ns;
+    const uint4 sp = live ? split[j] : make_uint4(0, 0, 0, 0);
+    if (lane == 0) nl[wave] = sp.z;
+    __syncthreads();
+    const uint32_t mx = max(max(nl[0], nl[1]), max(nl[2], nl[3]));  // most pieces in the block
+    const uint32_t nload = (mx + 63) / 64;
+    uint32_t lev = 0;  // tree levels: ceil(log2(min(mx, 64))) -- 1 for the usual 2-piece buckets
+    while ((1u << lev) < min(mx, 64u)) lev++;
+    Xyzz<F> v = xyzz_inf<F>();
+    for (uint32_t step = 0; step < nload + lev; step++) {
+      Xyzz<F> q;
+      bool act = false;
+      if (step < nload) {
+        const uint32_t pc = lane + 64u * step;
+        if (pc < sp.z) {
+          q = ld_xyzz<G>(xpts + (size_t)(sp.y + pc) * XW);
+          act = !xyzz_is_inf(q);
+        }
+      } else {
+        const uint32_t sz = (1u << (lev - 1)) >> (step - nload);
+        if (lane >= sz && lane < 2 * sz) sh[wave][lane - sz] = v;
+        __syncthreads();
+        if (lane < sz) {
+          q = sh[wave][lane];
+          act = !xyzz_is_inf(q);
+        }
+      }
+      if (act) v = xyzz_is_inf(v) ? q : br_add<G>(v, q);
+      if (step >= nload) __syncthreads();
+    }
+    if (live && lane == 0) st_xyzz<G>(buckets + (size_t)sp.x * XW, v);
   }
-  st_xyzz<G>(buckets + (size_t)b * XW, sum);
 }
 
 template <class G>
@@ -1530,10 +1760,15 @@ __global__ void __launch_bounds__(256) k_msm_accN_coop(const uint32_t* __restric
 __device__ __forceinline__ uint32_t insert_bit(uint32_t t, int bit) {
   return (((t >> bit) << (bit + 1)) | (1u << bit) | (t & ((1u << bit) - 1)));
 }
-#define ZK_BR_WPE 4  // at most 4 waves/SIMD: the compiler may use up to 128 VGPRs
+#define ZK_BR_WPE 4  // at most 4 waves/SIMD
+// minimum waves/SIMD the register allocation must allow (ZK_BR_MINW 4: <= 128
+// VGPRs, so a reduction wave fits beside three accumulation waves)
+#ifndef ZK_BR_MINW
+#define ZK_BR_MINW 1
+#endif
 
 template <class G, bool BITS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE))) k_msm_br(const uint32_t* __restrict__ src0, const uint32_t* __restrict__ src1,
                                                 const uint32_t* __restrict__ bstart, int lb, int hb, int W, int sr,
                                                 int sc, int sb, int segt, uint32_t* __restrict__ out0,
                                                 uint32_t* __restrict__ out1) {
@@ -1646,7 +1881,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_
 // jobs (4 folds + 6 levels each), and the bucket reduction runs beside the
 // other lane's accumulation, where wasted VALU issue is what it costs.
 template <class G>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, ZK_BR_WPE))) k_msm_br_strip(const uint32_t* __restrict__ buckets,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZK_BR_MINW, ZK_BR_WPE))) k_msm_br_strip(const uint32_t* __restrict__ buckets,
                                                       const uint32_t* __restrict__ bstart, int lb, int hb, int W,
                                                       int sr, int sc, int mc, uint32_t* __restrict__ outC,
                                                       uint32_t* __restrict__ outD) {
@@ -2293,41 +2528,6 @@ static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, size_t n, 
 }
 
 template <int C, bool BAL>
-static void launch_p1_fused(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t NH,
-                            uint32_t lob, uint32_t CS, uint32_t nf, uint32_t* cnt1, uint32_t* okey, uint32_t* oval,
-                            bool scatter) {
-  // sub-tiles of 1024 scalars when their LDS fits (c >= 15: W <= 17), else
-  // 256: 2^26 table MSM sort 12.2 -> 10.4 ms isolated (P1 runs 6 -> 24
-  // entries per bin)
-  constexpr int W = msm_windows(C);
-  if (scatter && rs_scatter_lds(NH, 1024 * W, 1024) <= 160 * 1024)
-    k_rs_p1f_scatter<C, 1024, BAL><<<nf, 1024, rs_scatter_lds(NH, 1024 * W, 1024), st>>>(sc, n, Wp, B, NH, lob, CS, nf,
-                                                                                    cnt1, okey, oval);
-  else if (scatter)
-    k_rs_p1f_scatter<C, RS_THREADS, BAL><<<nf, RS_THREADS, rs_scatter_lds(NH, RS_THREADS * W), st>>>(
-        sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval);
-  else
-    k_rs_p1f_count<C, BAL><<<nf, RS_THREADS, NH * 4, st>>>(sc, n, Wp, B, NH, lob, CS, nf, cnt1);
-}
-static int p1_fused(int c, bool bal, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t NH,
-                    uint32_t lob, uint32_t CS, uint32_t nf, uint32_t* cnt1, uint32_t* okey, uint32_t* oval,
-                    bool scatter) {
-  switch (c) {
-#define ZK_C(CC)                                                                                  \
-  case CC:                                                                                        \
-    if (bal) launch_p1_fused<CC, true>(st, sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval, scatter); \
-    else launch_p1_fused<CC, false>(st, sc, n, Wp, B, NH, lob, CS, nf, cnt1, okey, oval, scatter);    \
-    break;
-    ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15) ZK_C(16) ZK_C(17) ZK_C(18) ZK_C(19) ZK_C(20) ZK_C(21) ZK_C(22)
-#undef ZK_C
-    default:
-      set_error("p1_fused: unsupported MSM window %d", c);
-      return ZKMI_EINVAL;
-  }
-  return 0;
-}
-
-template <int C, bool BAL>
 static void launch_small_sort(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t K,
                               uint32_t* cnt, uint32_t* cursor, uint32_t* bstart, uint32_t* sval) {
   const unsigned g = (unsigned)((n + 255) / 256);
@@ -2367,8 +2567,7 @@ struct zkmi_msm_job {
   int sb = 1;                   // segments per bit sum (added on the host)
   hipStream_t st = nullptr;     // lane stream the D2H of `host` is queued on
   zkmi_comm* comm = nullptr;    // sharded MSM: bit sums of every rank are summed
-  size_t status_words = 0;      // sharded: status block after the bit sums (per rank)
-  bool exchanged = false;       // sharded over RCCL: the data all-gather is queued
+  bool exchanged = false;       // sharded over RCCL: the all-gather is queued
 };
 
 namespace zk {
@@ -2389,6 +2588,7 @@ static int get_lane(zkmi_ctx* ctx, MsmLane** out) {
       return ZKMI_EHIP;
     }
     ctx->lanes.push_back(l);
+    ctx->nstreams++;
   }
   *out = ctx->lanes[i];
   return 0;
@@ -2421,13 +2621,88 @@ static MsmPlan msm_plan(const zkmi_ctx* ctx, const zkmi_bases* tb, size_t n) {
 static bool same_plan(const MsmPlan& a, const MsmPlan& b) {
   return a.c == b.c && a.p == b.p && a.W == b.W && a.bal == b.bal;
 }
+// one lane per bucket (k_acc_items_*): table plans of >= 2^18 buckets, one or
+// two windows (the bin sort makes the items).  (Small table MSMs -- the
+// configs[0] proof's ~8K-point MSMs, 2^12 buckets -- on this path with cap 8
+// or 16: resident prove 2.95-3.02 / 3.10-3.35 ms against 2.74-2.86 ms on the
+// chunked path, round 5; they stay chunked.)
+static bool items_plan(const MsmPlan& P) { return P.K >= ITEMS_MIN_K && P.W <= 2 && P.c >= 12 && P.c <= 22; }
+// Piece cap of the items: no lane may run much longer than the kernel's share
+// per resident lane (~M / (CUs x 768 lanes)), or its chain becomes the tail;
+// buckets above it (witness-like 0/1 scalars, small scalars) are split and
+// their pieces summed after (k_split_combine).
+static uint32_t item_cap(const zkmi_ctx* ctx, const MsmPlan& P) {
+  const size_t share = P.Mmax / ((size_t)ctx->num_cus * 768 * 2);
+  // (2^20 tables: 64, 2^26: 1024)
+  uint32_t cap = 64;
+  while (cap < share && cap < ITEM_CAP_MAX) cap <<= 1;
+  return cap;
+}
+// Bin-sort geometry (k_bs_*): NH bins of NLO = 2^lob keys; A / B chunks of CS
+// scalars, super-chunks of 2^scs chunks; C / D tiles of <= C2 entries, T2max
+// of them at most.  Counter block: bin totals [NH], item counters [16],
+// super-chunk totals [BS_NSC][NH], class histogram and cursors
+// [2][ITEM_CAP_MAX + 1].  A lane holds two blocks and alternates them; each
+// sort's first kernel clears the other block for the next sort (its last
+// readers, the previous MSM's accumulation and piece sums, ran before on the
+// same stream), so a sort needs no memset launch.
+struct BsGeom {
+  uint32_t lob, NLO, NH, CS, nf, scs, C2, T2max;
+  size_t nmain;  // items: NH * NLO main slots
+  size_t ctr_words() const { return (size_t)NH + 16 + (size_t)BS_NSC * NH + 2 * (ITEM_CAP_MAX + 1); }
+  uint32_t* ghist(uint32_t* ctr) const { return ctr + NH + 16 + (size_t)BS_NSC * NH; }
+};
+static BsGeom bs_geom(const MsmPlan& P, size_t n) {
+  BsGeom g;
+  uint32_t kb = 0;
+  while ((1u << kb) < P.K) kb++;
+  // lo digit: 11 bits for large key spaces; small ones keep >= 16 bins for P2's
+  // parallelism and >= 64 keys per bin (the items' wave-major layout)
+  g.lob = kb >= 15 ? std::min(11u, kb) : std::max(6u, kb > 4 ? kb - 4 : 0u);
+  g.NLO = 1u << g.lob;
+  g.NH = (P.K + g.NLO - 1) >> g.lob;
+  g.CS = 1024u * (uint32_t)std::max<size_t>(1, (n + 1024ull * 2048 - 1) / (1024ull * 2048));
+  g.nf = (uint32_t)std::max<size_t>(1, (n + g.CS - 1) / g.CS);
+  g.scs = 0;
+  while (((size_t)g.nf + (1u << g.scs) - 1) >> g.scs > BS_NSC) g.scs++;
+  const size_t C2B = P.Mmax < ((size_t)1 << 22) ? 4096 : 16384;  // small sorts: more, shorter tiles
+  g.C2 = (uint32_t)(C2B * std::max<size_t>(1, (P.Mmax + C2B * C2B - 1) / (C2B * C2B)));
+  g.T2max = (uint32_t)((P.Mmax + g.C2 - 1) / g.C2) + g.NH;
+  g.nmain = (size_t)g.NH * g.NLO;
+  return g;
+}
+constexpr int BS_ST = 4096;  // k_bs_scatter2 entries per LDS sub-tile
+static size_t bs_lds_scatter2(const BsGeom& g) { return rs_scatter_lds(g.NLO, BS_ST) + (2 * (size_t)g.NH + 2) * 4; }
 
-// exclusive scan of a[0..len) in place; *total = sum (bsums: len/1024 + 1 words)
-static void scan_excl(hipStream_t st, uint32_t* a, size_t len, uint32_t* bsums, uint32_t* total) {
-  uint32_t nb = (uint32_t)((len + 1023) / 1024);
-  k_scan_blocks<<<nb, 256, 0, st>>>(a, (uint32_t)len, a, bsums);
-  k_scan_top<<<1, 1024, 0, st>>>(bsums, nb, total);
-  k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
+template <int C, bool BAL>
+static void launch_bs_p1(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, const BsGeom& g,
+                         uint32_t* ctr, uint32_t* next_ctr, uint32_t* choff, uint32_t* okey, uint32_t* oval,
+                         bool scatter) {
+  constexpr int W = msm_windows(C);
+  uint32_t* bintot = ctr;
+  uint32_t* sctot = ctr + g.NH + 16;
+  if (scatter)
+    k_bs_scatter1<C, 256, BAL><<<g.nf, 256, rs_scatter_lds(g.NH, 256 * W), st>>>(
+        sc, n, Wp, B, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff, okey, oval);
+  else
+    k_bs_count<C, BAL><<<g.nf, 256, g.NH * 4, st>>>(sc, n, Wp, B, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff,
+                                                    next_ctr, (uint32_t)g.ctr_words());
+}
+static int bs_p1(int c, bool bal, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, const BsGeom& g,
+                 uint32_t* ctr, uint32_t* next_ctr, uint32_t* choff, uint32_t* okey, uint32_t* oval, bool scatter) {
+  switch (c) {
+#define ZK_C(CC)                                                                                  \
+  case CC:                                                                                        \
+    if (bal) launch_bs_p1<CC, true>(st, sc, n, Wp, B, g, ctr, next_ctr, choff, okey, oval, scatter); \
+    else launch_bs_p1<CC, false>(st, sc, n, Wp, B, g, ctr, next_ctr, choff, okey, oval, scatter);    \
+    break;
+    ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15) ZK_C(16) ZK_C(17) ZK_C(18) ZK_C(19) ZK_C(20) ZK_C(21) ZK_C(22)
+#undef ZK_C
+    default:
+      set_error("bin sort: unsupported MSM window %d", c);
+      return ZKMI_EINVAL;
+  }
+  return 0;
 }
 
 // Timing ablation for development only (tools/headline_loop.py): ZKMI_DEBUG_SKIP
@@ -2470,25 +2745,19 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   const uint32_t C2b = std::max(8192u, 4u << lob);  // >= 4 entries per lo bin per tile
   const uint32_t C2 = C2b * (uint32_t)std::max<size_t>(1, (Mmax + (size_t)C2b * 8192 - 1) / ((size_t)C2b * 8192));
   const uint32_t T2max = (uint32_t)((Mmax + C2 - 1) / C2) + NH;
-  // fused P1: chunks of CS scalars (~2K chunks at most)
-  const uint32_t CS = 1024u * (uint32_t)std::max<size_t>(1, (n + 1024ull * 2048 - 1) / (1024ull * 2048));
-  const uint32_t nf = (uint32_t)std::max<size_t>(1, (n + CS - 1) / CS);
-  const size_t len1 = (size_t)NH * std::max(nc1, nf), len2 = (size_t)T2max << lob;
+  const size_t len1 = (size_t)NH * nc1, len2 = (size_t)T2max << lob;
   int32_t* digits;
   uint32_t *bstart, *sval, *cnt1, *okey, *oval, *binstart, *tstart, *cnt2, *bsums, *tot;
-  const bool fused = P.c >= 12 && P.c <= 22;  // P1 reads the scalars (k_rs_p1f_*)
+  const bool fused = P.c >= 12 && P.c <= 22;  // the sort reads the scalars (k_bs_*, k_ss_*)
   digits = nullptr;
   if (!fused) ZK_TRY(ws.get("msm_digits", Mmax * 4, (void**)&digits));
   ZK_TRY(ws.get("msm_bstart", (size_t)(P.K + 1) * 4, (void**)&bstart));
   ZK_TRY(ws.get("msm_sval", Mmax * 4, (void**)&sval));
-  ZK_TRY(ws.get("msm_okey", Mmax * 4, (void**)&okey));
-  ZK_TRY(ws.get("msm_oval", Mmax * 4, (void**)&oval));
-  ZK_TRY(ws.get("msm_cnt1", len1 * 4, (void**)&cnt1));
-  ZK_TRY(ws.get("msm_cnt2", len2 * 4, (void**)&cnt2));
-  ZK_TRY(ws.get("msm_binstart", (size_t)(NH + 1) * 4, (void**)&binstart));
-  ZK_TRY(ws.get("msm_tstart", (size_t)(NH + 1) * 4, (void**)&tstart));
-  ZK_TRY(ws.get("msm_bsums", ((std::max(len1, len2) + 1023) / 1024) * 4 + 16, (void**)&bsums));
-  ZK_TRY(ws.get("msm_tot", 64, (void**)&tot));
+  const bool small = fused && Mmax <= SMALL_SORT_MAX && !items_plan(P) && P.K <= (1u << 16);
+  if (!small) {
+    ZK_TRY(ws.get("msm_okey", Mmax * 4, (void**)&okey));
+    ZK_TRY(ws.get("msm_oval", Mmax * 4, (void**)&oval));
+  }
   if (ctx->msm_fork) {
     ZK_HIP(hipStreamWaitEvent(st, ctx->msm_fork, 0));
   } else {
@@ -2502,7 +2771,61 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   }
   lane->debug_sorted = 1;
   ScopedKernelTimer tm(ctx, "msm_sort", st);
-  if (fused && Mmax <= SMALL_SORT_MAX) {
+  if (fused && !small) {
+    // bin sort (k_bs_*): memset + 4 kernels; items for one-lane-per-bucket plans
+    const BsGeom g = bs_geom(P, n);
+    const bool items = items_plan(P);
+    uint32_t *ctr2, *choff, *thist;
+    uint4 *it = nullptr, *split = nullptr, *stage = nullptr;
+    const size_t cw = g.ctr_words();
+    ZK_TRY(ws.get("msm_bs_ctr", 2 * cw * 4, (void**)&ctr2));
+    // a new buffer, another geometry (the blocks' layout moves) or an
+    // interrupted sort: both blocks cleared
+    if (ctr2 != lane->bs_ctr || cw != lane->bs_ctr_words || lane->bs_dirty) {
+      ZK_HIP(hipMemsetAsync(ctr2, 0, 2 * cw * 4, st));
+      lane->bs_ctr = ctr2;
+      lane->bs_ctr_words = cw;
+      lane->bs_parity = 0;
+    }
+    lane->bs_dirty = true;  // until every kernel of this sort is queued
+    uint32_t* ctr = ctr2 + (size_t)lane->bs_parity * cw;
+    uint32_t* next_ctr = ctr2 + (size_t)(lane->bs_parity ^ 1) * cw;
+    ZK_TRY(ws.get("msm_bs_choff", (size_t)g.nf * g.NH * 4, (void**)&choff));
+    ZK_TRY(ws.get("msm_bs_thist", (size_t)g.T2max * g.NLO * 4, (void**)&thist));
+    ItemsOut io{nullptr, (uint32_t)g.nmain, 0, ctr + g.NH, nullptr, nullptr, g.ghist(ctr)};
+    if (items) {
+      io.cap = item_cap(ctx, P);
+      ZK_TRY(ws.get("msm_items", (g.nmain + (Mmax + io.cap - 1) / io.cap) * 16, (void**)&it));
+      ZK_TRY(ws.get("msm_split", ((Mmax + io.cap - 1) / io.cap + 1) * 16, (void**)&split));
+      ZK_TRY(ws.get("msm_items_stage", g.nmain * 16, (void**)&stage));
+      io.items = it;
+      io.split = split;
+      io.stage = stage;
+    }
+    ZK_TRY(bs_p1(P.c, P.bal, st, d_scalars, n, P.W, P.B, g, ctr, next_ctr, choff, okey, oval, false));
+    ZK_TRY(bs_p1(P.c, P.bal, st, d_scalars, n, P.W, P.B, g, ctr, next_ctr, choff, okey, oval, true));
+    ZK_HIP(hipEventRecord(lane->consumed, st));
+    ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
+    const uint32_t gt = ((g.T2max + 7) / 8) * 8;  // XCD-mapped grid (rs_xcd_tile)
+    k_bs_count2<<<gt, 256, (g.NLO + 2 * g.NH + 2 + 4) * 4, st>>>(okey, ctr, g.NH, g.lob, g.C2, g.T2max, thist);
+    if (items) {
+      k_bs_scatter2<BS_ST, true><<<gt, 256, bs_lds_scatter2(g), st>>>(okey, oval, ctr, g.NH, g.lob, g.C2, g.T2max,
+                                                                     P.K, thist, sval, bstart, io);
+      k_items_place<<<g.NH, 256, 0, st>>>(stage, g.NLO, io.cap, io.ghist, io.ghist + ITEM_CAP_MAX + 1, it,
+                                          (uint32_t)g.nmain);
+    } else {
+      k_bs_scatter2<BS_ST, false><<<gt, 256, bs_lds_scatter2(g), st>>>(okey, oval, ctr, g.NH, g.lob, g.C2, g.T2max,
+                                                                      P.K, thist, sval, bstart, io);
+    }
+    lane->bs_cur = ctr;  // the accumulation phases of this sort read its item counters
+    lane->bs_parity ^= 1;
+    lane->bs_dirty = false;
+    ZK_HIP(hipGetLastError());
+    *out_sval = sval;
+    *out_bstart = bstart;
+    return 0;
+  }
+  if (small) {
     uint32_t *scnt, *scur;
     ZK_TRY(ws.get("msm_ss_cnt", (size_t)P.K * 4, (void**)&scnt));
     ZK_TRY(ws.get("msm_ss_cursor", (size_t)P.K * 4, (void**)&scur));
@@ -2515,7 +2838,14 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
     *out_bstart = bstart;
     return 0;
   }
-  if (!fused) {
+  // windows c < 12: digits array + two-pass radix sort
+  ZK_TRY(ws.get("msm_cnt1", len1 * 4, (void**)&cnt1));
+  ZK_TRY(ws.get("msm_cnt2", len2 * 4, (void**)&cnt2));
+  ZK_TRY(ws.get("msm_binstart", (size_t)(NH + 1) * 4, (void**)&binstart));
+  ZK_TRY(ws.get("msm_tstart", (size_t)(NH + 1) * 4, (void**)&tstart));
+  ZK_TRY(ws.get("msm_bsums", ((std::max(len1, len2) + 1023) / 1024) * 4 + 16, (void**)&bsums));
+  ZK_TRY(ws.get("msm_tot", 64, (void**)&tot));
+  {
     ZK_TRY(dispatch_digits(P.c, st, d_scalars, n, P.p, P.W, P.bal, digits));
     ZK_HIP(hipEventRecord(lane->consumed, st));
     ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
@@ -2527,19 +2857,11 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
     k_scan_add<<<(unsigned)((len + 255) / 256), 256, 0, st>>>(a, (uint32_t)len, bsums, nullptr);
   };
   const uint32_t ne = (uint32_t)P.ne;
-  if (fused) {
-    ZK_TRY(p1_fused(P.c, P.bal, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, nullptr, nullptr, false));
-    scan(cnt1, (size_t)NH * nf, &tot[0]);
-    ZK_TRY(p1_fused(P.c, P.bal, st, d_scalars, n, P.W, P.B, NH, lob, CS, nf, cnt1, okey, oval, true));
-    ZK_HIP(hipEventRecord(lane->consumed, st));
-    ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
-  } else {
-    k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1, cnt1);
-    scan(cnt1, len1, &tot[0]);
-    k_rs_p1_scatter<4096><<<nc1, RS_THREADS, rs_scatter_lds(NH, 4096), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1,
-                                                                             cnt1, okey, oval);
-  }
-  k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, fused ? nf : nc1, NH, &tot[0], C2, binstart, tstart);
+  k_rs_p1_count<<<nc1, RS_THREADS, NH * 4, st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1, cnt1);
+  scan(cnt1, len1, &tot[0]);
+  k_rs_p1_scatter<4096><<<nc1, RS_THREADS, rs_scatter_lds(NH, 4096), st>>>(digits, Mmax, ne, P.B, NH, lob, C1, nc1,
+                                                                           cnt1, okey, oval);
+  k_rs_tiles<<<1, 1024, 0, st>>>(cnt1, nc1, NH, &tot[0], C2, binstart, tstart);
   // cnt2 needs no clearing: tiles t < tstart[NH] write all their counts, and
   // the stale tail after them only reaches the (unused) scan total
   const uint32_t g2 = ((T2max + 7) / 8) * 8;  // XCD-mapped grid (rs_xcd_tile)
@@ -2582,7 +2904,10 @@ static BrGeom br_geom(const MsmPlan& P, bool g2) {
   // buckets folded per lane before the tree: G1 8 (16 with two 512-bucket
   // columns per wave measured slower: 2^20 one lane 0.38 -> 0.46 ms); G2 16
   // (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
-  const int fold = g2 ? 16 : 8;
+#ifndef ZK_BR_FOLD_G1
+#define ZK_BR_FOLD_G1 8
+#endif
+  const int fold = g2 ? 16 : ZK_BR_FOLD_G1;
   BrGeom g;
   g.mode = P.hb >= 9 ? 1 : 0;
   g.segt = 256;
@@ -2598,42 +2923,65 @@ static BrGeom br_geom(const MsmPlan& P, bool g2) {
   return g;
 }
 
-// Queue the hand-over of a job's bit sums (W*(bb+1)*sb XYZZ terms, `words`
-// u32 at d_sums) on stream st (the lane stream): for a sharded MSM over RCCL, first the
-// all-gather of every rank's bit sums (comm stream, ordered after the lane's
-// work), then the D2H into the job's pinned buffer and the job's event.
-// Plan signature word of a sharded job's status block (with sb and W).
-static uint32_t shard_sig0(const zkmi_msm_job* job) {
-  return 0x5A000000u | ((uint32_t)job->g2 << 16) | ((uint32_t)job->c << 8) | (uint32_t)job->bb;
+// Sharded MSMs hand over exactly SHARD_PAYLOAD_WORDS u32 per rank: a status
+// block [failure flag, plan signature (g2, c, bit sums), segments, windows]
+// and the rank's bit sums after it.  The size is the same on every rank
+// whatever its plan, inputs or local failure, so every sharded submit is one
+// collective of one size on every rank and no rank can wait in a collective
+// another rank skips; msm_wait fails on every rank when the plans of the
+// non-empty shards differ.  36,864 words hold every table plan (<= 22.5K
+// words) and the plain plans of windows <= 20 (<= 34.6K words for G2).
+constexpr size_t SHARD_PAYLOAD_WORDS = 36864;
+static uint32_t shard_sig0(int g2, int c, int bb) {
+  return 0x5A000000u | ((uint32_t)g2 << 16) | ((uint32_t)c << 8) | (uint32_t)bb;
+}
+__global__ void k_put_words(uint32_t* __restrict__ dst, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  if (threadIdx.x < 4) dst[threadIdx.x] = threadIdx.x == 0 ? w0 : threadIdx.x == 1 ? w1 : threadIdx.x == 2 ? w2 : w3;
 }
 
-static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, hipStream_t st, zkmi_msm_job* job, const uint32_t* d_sums,
+// Queue the hand-over of a job's bit sums on stream st (the lane stream):
+// d_buf holds a SHARD_STATUS_WORDS status block, then `words` u32 of bit sums
+// (W*(bb+1)*sb XYZZ terms; 0 for an empty shard).  Unsharded: the D2H of the
+// bit sums into the job's pinned buffer and the job's event.  Sharded: the
+// status block first; over RCCL the all-gather of every rank's payload (comm
+// stream, ordered after the lane's work) and one strided D2H of every rank's
+// status block + bit sums; over a host transport the D2H of this rank's part
+// (msm_wait exchanges it).
+static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, hipStream_t st, zkmi_msm_job* job, uint32_t* d_buf,
                               size_t words) {
-  const int nr = job->comm ? job->comm->nranks : 1;
-  const bool dev_gather = job->comm && job->comm->kind == ZKMI_COMM_RCCL;
-  const uint32_t* src = d_sums;
-  if (job->comm) {  // sharded: a status block ends this rank's payload (d_sums has room):
-    // word 0 = failure flag (0 here), words 1..3 = the plan signature msm_wait compares
-    uint32_t* stw = const_cast<uint32_t*>(d_sums) + words;
-    const uint32_t sig[3] = {shard_sig0(job), (uint32_t)job->sb, (uint32_t)job->W};
-    ZK_HIP(hipMemsetAsync(stw, 0, 4, st));
-    for (int i = 0; i < 3; i++) ZK_HIP(hipMemsetD32Async((hipDeviceptr_t)(stw + 1 + i), (int)sig[i], 1, st));
-    words += SHARD_STATUS_WORDS;
-    job->status_words = SHARD_STATUS_WORDS;
-  }
-  if (dev_gather) {
-    uint32_t* gathered;
-    ZK_TRY(lane->ws.get("msm_gathered", (size_t)nr * words * 4, (void**)&gathered));
-    ZK_TRY(comm_allgather_device(job->comm, st, d_sums, gathered, words * 4));
-    job->exchanged = true;
-    src = gathered;
-  }
-  job->host_words = words;
-  const size_t host_words = dev_gather ? (size_t)nr * words : words;
   ZK_HIP(hipEventCreateWithFlags(&job->done, hipEventDisableTiming));
-  ZK_TRY(ctx_pinned_get(ctx, host_words * 4, (void**)&job->host));
-  job->st = st;  // from here on the pinned buffer may have a copy in flight
-  ZK_HIP(hipMemcpyAsync(job->host, src, host_words * 4, hipMemcpyDeviceToHost, st));
+  if (!job->comm) {
+    job->host_words = words;
+    ZK_TRY(ctx_pinned_get(ctx, words * 4, (void**)&job->host));
+    job->st = st;  // from here on the pinned buffer may have a copy in flight
+    ZK_HIP(hipMemcpyAsync(job->host, d_buf + SHARD_STATUS_WORDS, words * 4, hipMemcpyDeviceToHost, st));
+    ZK_HIP(hipEventRecord(job->done, st));
+    return 0;
+  }
+  const int nr = job->comm->nranks;
+  const bool empty = words == 0;
+  k_put_words<<<1, 64, 0, st>>>(d_buf, 0u, shard_sig0(job->g2, empty ? 0 : job->c, empty ? 0 : job->bb),
+                                empty ? 0u : (uint32_t)job->sb, empty ? 0u : (uint32_t)job->W);
+  ZK_HIP(hipGetLastError());
+  // what msm_wait reads of each rank: status + bit sums of this rank's plan
+  // (the plan every non-empty shard must share); everything for an empty shard
+  const size_t width = empty ? SHARD_PAYLOAD_WORDS : SHARD_STATUS_WORDS + words;
+  if (job->comm->kind == ZKMI_COMM_RCCL) {
+    uint32_t* gathered;
+    ZK_TRY(lane->ws.get("msm_gathered", (size_t)nr * SHARD_PAYLOAD_WORDS * 4, (void**)&gathered));
+    ZK_TRY(comm_allgather_device(job->comm, st, d_buf, gathered, SHARD_PAYLOAD_WORDS * 4));
+    job->exchanged = true;
+    job->host_words = width;
+    ZK_TRY(ctx_pinned_get(ctx, (size_t)nr * width * 4, (void**)&job->host));
+    job->st = st;
+    ZK_HIP(hipMemcpy2DAsync(job->host, width * 4, gathered, SHARD_PAYLOAD_WORDS * 4, width * 4, nr,
+                            hipMemcpyDeviceToHost, st));
+  } else {
+    job->host_words = SHARD_PAYLOAD_WORDS;  // the host all-gather sends the whole payload
+    ZK_TRY(ctx_pinned_get(ctx, SHARD_PAYLOAD_WORDS * 4, (void**)&job->host));
+    job->st = st;
+    ZK_HIP(hipMemcpyAsync(job->host, d_buf, width * 4, hipMemcpyDeviceToHost, st));
+  }
   ZK_HIP(hipEventRecord(job->done, st));
   return 0;
 }
@@ -2653,47 +3001,22 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   const int W = P.W, bb = P.bb, lb = P.lb, hb = P.hb;
   const size_t Mmax = P.Mmax;
   const uint32_t tn = (uint32_t)n, tskip = P.p > 1 ? (uint32_t)(tb->n - n) : 0u;
-  uint32_t *buckets, *flags;
+  uint32_t* buckets;
   ZK_TRY(ws.get("msm_buckets", (size_t)K * XW * 4, (void**)&buckets));
-  ZK_TRY(ws.get("msm_flags", 64 * 4, (void**)&flags));
-  ZK_HIP(hipMemsetAsync(flags, 0, 64 * 4, st));
-  uint32_t *xkey, *xvalid, *xpts, *ykey, *yvalid, *ypts;
-  size_t xl;  // length of the partial list the segmented cascade starts from
-  if (K >= ITEMS_MIN_K && W <= 2) {  // table plans (one window of many buckets)
-    // one lane per bucket (k_acc_items); partials only for buckets > cap
-    // Piece cap: no lane may run much longer than the kernel's share per
-    // resident lane (~M / (CUs x 768 lanes)), or its chain becomes the tail;
-    // buckets above it (low buckets that also take the short top window,
-    // witness-like 0/1 scalars) are split and their pieces summed after.
-    const size_t share = Mmax / ((size_t)ctx->num_cus * 768 * 2);
-    uint32_t cap = 64;
-    while (cap < share && cap < ITEM_CAP_MAX) cap <<= 1;
-    const size_t items_max = (size_t)K + (Mmax + cap - 1) / cap;
-    xl = 2 * ((Mmax + cap - 1) / cap) + 2;
-    uint32_t *hist, *cursor, *nitems, *hv, *bsums;
-    uint4* items;
-    ZK_TRY(ws.get("msm_it_hist", (ITEM_CAP_MAX + 1) * 4, (void**)&hist));
-    ZK_TRY(ws.get("msm_it_cursor", (ITEM_CAP_MAX + 1) * 4, (void**)&cursor));
-    ZK_TRY(ws.get("msm_it_n", 64, (void**)&nitems));
-    ZK_TRY(ws.get("msm_it_hv", ((size_t)K + 1) * 4, (void**)&hv));
-    ZK_TRY(ws.get("msm_it_bsums", ((size_t)K / 1024 + 2) * 4, (void**)&bsums));
+  if (items_plan(P)) {  // table plans (one window of many buckets)
+    // one lane per bucket (k_acc_items); the items, the split list and their
+    // counters come from the sort (k_bs_scatter2)
+    const BsGeom g = bs_geom(P, n);
+    const uint32_t cap = item_cap(ctx, P);
+    const size_t npieces = (Mmax + cap - 1) / cap;
+    const size_t items_max = g.nmain + npieces;
+    uint32_t* ctr = lane->bs_cur;  // the counter block of this lane's last sort
+    uint32_t* xpts;
+    uint4 *items, *split;
     ZK_TRY(ws.get("msm_items", items_max * 16, (void**)&items));
-    ZK_TRY(ws.get("msm_xkey", xl * 4 + 64, (void**)&xkey));
-    ZK_TRY(ws.get("msm_xvalid", xl * 4 + 64, (void**)&xvalid));
-    ZK_TRY(ws.get("msm_xpts", (xl + 2) * XW * 4, (void**)&xpts));
-    ZK_TRY(ws.get("msm_ykey", xl * 4 + 64, (void**)&ykey));
-    ZK_TRY(ws.get("msm_yvalid", xl * 4 + 64, (void**)&yvalid));
-    ZK_TRY(ws.get("msm_ypts", (xl + 2) * XW * 4, (void**)&ypts));
-    if (!((debug_skip() & 1) && lane->debug_sorted == 2)) {
-      lane->debug_sorted = 2;
-      ScopedKernelTimer tm(ctx, "msm_items_plan", st);
-      ZK_HIP(hipMemsetAsync(hist, 0, (ITEM_CAP_MAX + 1) * 4, st));
-      const unsigned ig = (K + 256 * ITEMS_IPT - 1) / (256 * ITEMS_IPT);
-      k_items_count<<<ig, 256, 0, st>>>(bstart, K, cap, hist, hv, &flags[0]);
-      scan_excl(st, hv, K, bsums, &nitems[1]);
-      k_items_offsets<<<1, 1, 0, st>>>(hist, cap, cursor, &nitems[0]);
-      k_items_scatter<<<ig, 256, 0, st>>>(bstart, K, cap, hv, cursor, items, &flags[0], xkey, xvalid, (uint32_t)xl);
-    }
+    ZK_TRY(ws.get("msm_split", (npieces + 1) * 16, (void**)&split));
+    ZK_TRY(ws.get("msm_xpts", (2 * npieces + 2) * XW * 4, (void**)&xpts));
+    const uint32_t* itc = ctr + g.NH;  // [0] overflow items, [1] partial slots, [2] split buckets
     // Table accumulations start in submission order across lanes: this one
     // waits for the previous one (on another lane) to end.  Run together, two
     // accumulations share the CUs and end together, and the lanes' tails and
@@ -2708,15 +3031,28 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     {
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
       auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
-      kern<<<(unsigned)((items_max + 255) / 256), 256, 0, st>>>(items, &nitems[0], sval, d_bases, tn,
-                                                                 tskip, buckets, xkey, xvalid, xpts);
+#ifndef ZK_ACC_LDS_KB
+#define ZK_ACC_LDS_KB 0
+#endif
+      // (ZK_ACC_LDS_KB: LDS reserved per accumulation workgroup, which caps
+      // its waves per SIMD -- 41 KB: three workgroups per CU)
+      kern<<<(unsigned)((items_max + 255) / 256), 256, (size_t)ZK_ACC_LDS_KB * 1024, st>>>(
+          items, &itc[0], (uint32_t)g.nmain, sval, d_bases, tn, tskip, buckets, xpts);
     }
     ZK_HIP(hipEventRecord(lane->acc_done, st));
     ctx->acc_last = lane;
     ScopedKernelTimer tm(ctx, "msm_accN", st);
-    k_items_combine<GB><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, cap, hv, buckets, xvalid, xpts, &nitems[1]);
+    auto comb = K <= CUTSUM_COOP_K ? k_split_combine<GS> : k_split_combine<GB>;  // small MSMs: latency-scheduled products
+    // one wave per split bucket in one pass up to 4096 of them (a small MSM's
+    // buckets at cap 8 are all split); the launch reads the count and exits
+    // when there is none
+    const size_t maxsplit = std::min<size_t>(K, npieces / 2 + 1);
+    comb<<<(unsigned)std::min<size_t>((maxsplit + 3) / 4, 1024), 256, 0, st>>>(split, &itc[2], xpts, buckets);
     ZK_HIP(hipGetLastError());
   } else {
+    uint32_t *flags, *xkey, *xvalid, *xpts, *ykey, *yvalid, *ypts;
+    ZK_TRY(ws.get("msm_flags", 64 * 4, (void**)&flags));
+    ZK_HIP(hipMemsetAsync(flags, 0, 64 * 4, st));
     // level 0: fixed-size chunks of the sorted list (sized from the upper bound
     // W*n so no host round-trip is needed; chunks past M exit at once).
     // Threads per CU: measured best at ~1024 for G1 (over-subscribing the
@@ -2725,7 +3061,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     const size_t acc_threads = (size_t)ctx->num_cus * tpc;
     uint32_t L = (uint32_t)std::max<size_t>(4, (Mmax + acc_threads - 1) / acc_threads);
     uint32_t nch = (uint32_t)((Mmax + L - 1) / L);
-    xl = 2 * (size_t)nch + 1;
+    const size_t xl = 2 * (size_t)nch + 1;  // length of the partial list the segmented cascade starts from
     ZK_TRY(ws.get("msm_xkey", xl * 4 + 64, (void**)&xkey));
     ZK_TRY(ws.get("msm_xvalid", xl * 4 + 64, (void**)&xvalid));
     ZK_TRY(ws.get("msm_xpts", (xl + 2) * XW * 4, (void**)&xpts));
@@ -2744,12 +3080,9 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
                                                                                    xpts, &flags[0]);
     else
       k_msm_cutsum<G><<<(K + 255) / 256, 256, 0, st>>>(bstart, K, L, buckets, xvalid, xpts, &flags[0]);
-  }
-  // segmented reduction of the remaining partials: level 1 pairs neighbours,
-  // deeper levels only carry heavy buckets; each level exits on device when
-  // the previous one left nothing open (no host round-trips)
-  {
-    ScopedKernelTimer tm(ctx, "msm_accN", st);
+    // segmented reduction of the remaining partials: level 1 pairs neighbours,
+    // deeper levels only carry heavy buckets; each level exits on device when
+    // the previous one left nothing open (no host round-trips)
     uint32_t cur_len = (uint32_t)xl;
     for (int level = 1; cur_len > 1; level++) {
       if (level >= 63) {
@@ -2784,7 +3117,10 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   const int sr = bg.sr, sc = bg.sc, sb = bg.sb;
   ZK_TRY(ws.get("msm_C", (size_t)W * (1u << hb) * sr * XW * 4, (void**)&Cb));
   ZK_TRY(ws.get("msm_D", (size_t)W * (1u << lb) * sc * XW * 4, (void**)&Db));
-  ZK_TRY(ws.get("msm_sums", ((size_t)W * (bb + 1) * sb * XW + SHARD_STATUS_WORDS) * 4, (void**)&sums));
+  // status block (sharded hand-over) + bit sums; a sharded payload is exchanged whole
+  const size_t sum_words = (size_t)W * (bb + 1) * sb * XW;
+  ZK_TRY(ws.get("msm_sums", std::max(sum_words + SHARD_STATUS_WORDS, job->comm ? SHARD_PAYLOAD_WORDS : 0) * 4,
+                (void**)&sums));
   if (!(debug_skip() & 4)) {
     ScopedKernelTimer tm(ctx, "msm_bucket_reduce", brs);
     uint32_t jobs2 = (uint32_t)W * (bb + 1) * sb;
@@ -2799,11 +3135,12 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       br1<<<(jobs1 + 3) / 4, 256, 0, brs>>>(buckets, nullptr, bstart, lb, hb, W, sr, sc, sb, 256, Cb, Db);
     }
     auto br2 = K <= CUTSUM_COOP_K ? k_msm_br<GS, true> : k_msm_br<GB, true>;
-    br2<<<(jobs2 + 3) / 4, 256, 0, brs>>>(Cb, Db, nullptr, lb, hb, W, sr, sc, sb, bg.segt, sums, nullptr);
+    br2<<<(jobs2 + 3) / 4, 256, 0, brs>>>(Cb, Db, nullptr, lb, hb, W, sr, sc, sb, bg.segt,
+                                          sums + SHARD_STATUS_WORDS, nullptr);
     ZK_HIP(hipGetLastError());
   }
   job->sb = sb;
-  return msm_queue_handover(ctx, lane, brs, job, sums, (size_t)W * (bb + 1) * sb * XW);
+  return msm_queue_handover(ctx, lane, brs, job, sums, sum_words);
 }
 
 static int msm_acc_any(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const zkmi_bases* tb, size_t offset, size_t n,
@@ -2923,12 +3260,13 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
   job->st = nullptr;  // the bit-sum copy has landed
   int rc = timer_flush(ctx, false);
   auto th0 = std::chrono::steady_clock::now();
-  // Sharded MSM: the bit sums of all nr ranks (rank-major, host_words each).
-  // Over RCCL they were all-gathered on the device before the D2H; over a
-  // host transport the exchange happens here.
+  // Sharded MSM: every rank's status block + bit sums (rank-major, host_words
+  // each).  Over RCCL they were all-gathered on the device before the D2H;
+  // over a host transport the exchange happens here.
   const int nr = job->comm ? job->comm->nranks : 1;
   const uint32_t* src = job->host;
   std::vector<uint32_t> gathered;
+  std::vector<int> live_ranks;  // ranks whose bit sums enter the sum
   if (job->comm && job->comm->kind == ZKMI_COMM_HOST) {
     gathered.resize((size_t)nr * job->host_words);
     const auto tx = std::chrono::steady_clock::now();
@@ -2944,39 +3282,67 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
     }
     src = gathered.data();
   }
-  if (job->comm) {  // every rank's status block: one failed rank fails the MSM everywhere
-    const uint32_t sig[3] = {shard_sig0(job), (uint32_t)job->sb, (uint32_t)job->W};
+  if (job->comm) {  // one failed rank fails the MSM everywhere; non-empty shards must share one plan
+    const uint32_t* ref = nullptr;
     for (int r = 0; r < nr; r++) {
-      const uint32_t* stw = src + (size_t)r * job->host_words + job->host_words - job->status_words;
+      const uint32_t* stw = src + (size_t)r * job->host_words;
       if (stw[0] != 0) {
         set_error("msm_sharded: rank %d failed while running its shard", r);
         msm_job_free(job);
         return ZKMI_EINVAL;
       }
-      if (memcmp(stw + 1, sig, sizeof(sig)) != 0) {
-        set_error("msm_sharded: rank %d ran another window plan (its shard's table or window setting changed "
-                  "on that rank only)", r);
+      if ((stw[1] >> 16) != (0x5A00u | (uint32_t)job->g2)) {
+        set_error("msm_sharded: rank %d runs a %s MSM (or is out of step)", r, job->g2 ? "G1" : "G2");
         msm_job_free(job);
         return ZKMI_EINVAL;
       }
+      if (((stw[1] >> 8) & 0xFF) == 0) continue;  // empty shard
+      if (!ref) {
+        ref = stw;
+      } else if (memcmp(ref + 1, stw + 1, 3 * sizeof(uint32_t)) != 0) {
+        set_error("msm_sharded: window plans differ between ranks (c %u/%u, windows %u/%u): use equal shards "
+                  "and the same fixed-base table and window setting on every rank",
+                  (ref[1] >> 8) & 0xFF, (stw[1] >> 8) & 0xFF, ref[3], stw[3]);
+        msm_job_free(job);
+        return ZKMI_EINVAL;
+      }
+      live_ranks.push_back(r);
     }
+    if (!ref) {  // every shard empty: the sum is infinity
+      memset(out, 0, PW * 4);
+      msm_job_free(job);
+      return rc;
+    }
+    job->c = (int)((ref[1] >> 8) & 0xFF);
+    job->bb = (int)(ref[1] & 0xFF);
+    job->sb = (int)ref[2];
+    job->W = (int)ref[3];
+    if ((size_t)job->W * (job->bb + 1) * job->sb * XW + SHARD_STATUS_WORDS > job->host_words) {
+      set_error("msm_sharded: the agreed plan does not fit the exchanged payload");
+      msm_job_free(job);
+      return ZKMI_EINVAL;
+    }
+  } else {
+    live_ranks.push_back(0);
   }
+  const size_t skip = job->comm ? SHARD_STATUS_WORDS : 0;  // status block before each rank's bit sums
   // terms: V_{c w + j} = U_{w,j} (j < c-1), then T_w at weight 2^{c w}
   // (each term arrives as sb segments per rank, all summed in the combine)
   int c = job->c, W = job->W, bb = job->bb, nbits = c * W, sb = job->sb;
+  const int nl = (int)live_ranks.size();
   const size_t TW = (size_t)XW * sb;  // words per term and rank
-  const size_t TA = TW * nr;          // words per term over all ranks
+  const size_t TA = TW * nl;          // words per term over the ranks summed
   std::vector<uint32_t> all((size_t)(nbits + W) * TA, 0);
-  for (int r = 0; r < nr; r++) {
-    const uint32_t* h = src + (size_t)r * job->host_words;
+  for (int q = 0; q < nl; q++) {
+    const uint32_t* h = src + (size_t)live_ranks[q] * job->host_words + skip;
     for (int w = 0; w < W; w++) {
       for (int j = 0; j < bb; j++)
-        memcpy(&all[((size_t)c * w + j) * TA + r * TW], &h[((size_t)w * (bb + 1) + j) * TW], TW * 4);
-      memcpy(&all[((size_t)nbits + w) * TA + r * TW], &h[((size_t)w * (bb + 1) + bb) * TW], TW * 4);
+        memcpy(&all[((size_t)c * w + j) * TA + q * TW], &h[((size_t)w * (bb + 1) + j) * TW], TW * 4);
+      memcpy(&all[((size_t)nbits + w) * TA + q * TW], &h[((size_t)w * (bb + 1) + bb) * TW], TW * 4);
     }
   }
-  if (!job->g2) msm_host_combine_g1(all.data(), nbits, W, c, sb * nr, out);
-  else msm_host_combine_g2(all.data(), nbits, W, c, sb * nr, out);
+  if (!job->g2) msm_host_combine_g1(all.data(), nbits, W, c, sb * nl, out);
+  else msm_host_combine_g2(all.data(), nbits, W, c, sb * nl, out);
   if (ctx->timer.enabled) {
     auto& t = ctx->timer.totals["msm_host_epilogue"];
     t.first += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
@@ -2993,146 +3359,69 @@ int msm_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_
   return msm_wait(job, out_affine);
 }
 
-// Point-sharded MSM (zkmi.h, multi-GPU): every rank agrees on one window plan
-// through a 32-byte header all-gather, runs its shard through the usual
-// pipeline, and the job hands over the bit sums of all ranks (msm_wait sums
-// them).  A rank with an empty shard contributes the same number of infinity
-// terms, so the collective still matches on every rank.
-// Failures never strand a peer inside a collective: every rank joins the
-// header exchange with its local validation result (hdr[6]) and all fail
-// together if one does; a rank that fails after the agreement still takes
-// part in the job's data exchange with its status word set
-// (comm_fail_exchange), so the others fail in msm_wait.
+// Point-sharded MSM (zkmi.h, multi-GPU): every rank runs its shard through
+// the usual pipeline with its own window plan and queues exactly one
+// fixed-size exchange (SHARD_PAYLOAD_WORDS per rank: status block + bit sums);
+// msm_wait checks the plans and sums the bit sums of every non-empty shard.
+// There is no plan-agreement collective: a rank whose plan, shard or local
+// checks differ still takes part in the same one exchange (with its failure
+// flag or its plan signature), so a mismatch fails msm_wait on every rank and
+// no rank can block in a collective the others skip.  (Round 4 agreed the
+// plan by a synchronous header all-gather on the first submit and cached it
+// per shard state; a rank whose cache missed alone -- its window or table
+// changed on that rank only -- entered the header exchange while its peers
+// entered the data exchange: a hang over RCCL.)
 int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                        zkmi_msm_job** out) {
   *out = nullptr;
   zkmi_ctx* ctx = comm->ctx;
-  int lrc = check_range(b, offset, n);
-  if (!lrc && b->ctx != ctx) {
+  int rc = check_range(b, offset, n);
+  if (!rc && b->ctx != ctx) {
     set_error("msm_sharded: base set belongs to another context than the communicator");
-    lrc = ZKMI_EINVAL;
+    rc = ZKMI_EINVAL;
   }
+  const int XW = b->g2 ? 64 : 32;
   MsmPlan P{};
-  BrGeom bg{};
-  if (!lrc) {
+  if (!rc) {
     P = msm_plan(ctx, b, n);
-    bg = br_geom(P, b->g2 != 0);
-    if (n) lrc = check_size(P, n);
+    if (n) rc = check_size(P, n);
   }
-  const std::string lerr = lrc ? std::string(zkmi_last_error()) : std::string();
-  const bool plan = !lrc && n;
-  // The plan of this (communicator, shard state) was agreed before: no control
-  // collective on this submit.  Every rank's plan signature still travels in
-  // its status block, so a plan that changed on one rank only fails msm_wait
-  // on every rank.
-  const zkmi_bases::AgreedPlan* hit = nullptr;
-  if (b) {
-    for (const auto& a : b->agreed)
-      if (a.comm_serial == comm->serial && a.n == n && a.window == ctx->msm_window && a.tc == b->tc &&
-          a.tp == b->tp && a.tw == b->tw && a.tbal == b->tbal) {
-        hit = &a;
-        break;
-      }
-  }
-  uint32_t agreed[4] = {0, 0, 0, 0};  // c, W, bb, sb of the shards (c = 0: all empty)
-  if (hit) {
-    memcpy(agreed, hit->hdr, sizeof(agreed));
-    if (plan && (agreed[0] != (uint32_t)P.c || agreed[1] != (uint32_t)P.W || agreed[2] != (uint32_t)P.bb ||
-                 agreed[3] != (uint32_t)bg.sb)) {
-      set_error("msm_sharded: this rank's window plan changed since it was agreed");
-      lrc = ZKMI_EINVAL;
+  if (!rc && n) {
+    const BrGeom bg = br_geom(P, b->g2 != 0);
+    if ((size_t)P.W * (P.bb + 1) * bg.sb * XW + SHARD_STATUS_WORDS > SHARD_PAYLOAD_WORDS) {
+      set_error("msm_sharded: window %d's bit sums exceed the sharded exchange (use a table or a window <= 20)", P.c);
+      rc = ZKMI_EINVAL;
     }
-  } else {
-    constexpr uint32_t MAGIC = 0x5A4B4D53u;
-    uint32_t hdr[8] = {MAGIC, b ? (uint32_t)b->g2 : 0u, plan ? (uint32_t)P.c : 0u, plan ? (uint32_t)P.W : 0u,
-                       plan ? (uint32_t)P.bb : 0u, plan ? (uint32_t)bg.sb : 0u, lrc ? 1u : 0u, 0u};
-    std::vector<uint32_t> all((size_t)8 * comm->nranks);
-    ZK_TRY(comm_allgather_host(comm, hdr, all.data(), sizeof(hdr)));
-    for (int r = 0; r < comm->nranks; r++) {
-      if (all[(size_t)8 * r + 6] == 0) continue;
-      if (lrc) set_error("%s", lerr.c_str());
-      else set_error("msm_sharded: rank %d failed its local checks", r);
-      return ZKMI_EINVAL;
-    }
-    const uint32_t* ref = nullptr;
-    for (int r = 0; r < comm->nranks; r++) {
-      const uint32_t* h = &all[(size_t)8 * r];
-      if (h[0] != MAGIC || h[1] != hdr[1]) {
-        set_error("msm_sharded: rank %d runs a %s MSM (or is out of step)", r, h[1] ? "G2" : "G1");
-        return ZKMI_EINVAL;
-      }
-      if (!h[2]) continue;  // empty shard
-      if (!ref) ref = h;
-      else if (memcmp(ref + 2, h + 2, 4 * sizeof(uint32_t)) != 0) {
-        set_error("msm_sharded: window plans differ between ranks (c %u/%u, windows %u/%u): use equal shards "
-                  "and the same fixed-base table choice on every rank", ref[2], h[2], ref[3], h[3]);
-        return ZKMI_EINVAL;
-      }
-    }
-    if (ref) memcpy(agreed, ref + 2, sizeof(agreed));
-    if (b->agreed.size() >= 16) b->agreed.erase(b->agreed.begin());
-    b->agreed.push_back({comm->serial, n, ctx->msm_window, b->tc, b->tp, b->tw, b->tbal,
-                         {agreed[0], agreed[1], agreed[2], agreed[3]}});
   }
   zkmi_msm_job* job = new_job(ctx, b, P, n);
   job->comm = comm;
-  if (!agreed[0]) {  // every shard empty: the sum is infinity, nothing to exchange
-    if (lrc) {
-      msm_job_free(job);
-      return lrc;  // (the peers exchange nothing either)
-    }
-    job->empty = true;
-    *out = job;
-    return 0;
-  }
-  job->empty = false;
-  job->c = (int)agreed[0];
-  job->W = (int)agreed[1];
-  job->bb = (int)agreed[2];
-  job->sb = (int)agreed[3];
-  const int XW = b->g2 ? 64 : 32;
-  const size_t words = (size_t)job->W * (job->bb + 1) * job->sb * XW;  // bit sums per rank
-  int rc = 0;
+  job->empty = false;  // every rank takes part in the exchange, empty shard or not
   MsmLane* lane = nullptr;
   // test hook (tests/host/test_sharded_msm.cpp): ZKMI_DEBUG_SHARD_FAIL=<rank>
-  // makes that rank fail after the plan agreement, before its exchange
+  // makes that rank fail before its exchange
   const char* dbg = getenv("ZKMI_DEBUG_SHARD_FAIL");
-  if (lrc) {  // local checks failed on a cached plan: join the exchange with a failure status
-    rc = lrc;
-  } else if (dbg && atoi(dbg) == comm->rank) {
+  if (!rc && dbg && atoi(dbg) == comm->rank) {
     set_error("msm_sharded: injected failure (ZKMI_DEBUG_SHARD_FAIL)");
     rc = ZKMI_EHIP;
-  } else if (n) {
+  }
+  if (!rc && n) {
     uint32_t *sval, *bstart;
     if (!(rc = get_lane(ctx, &lane)) && !(rc = msm_sort_phase(ctx, lane, P, (const uint32_t*)d_scalars, n, &sval,
                                                                &bstart)))
       rc = msm_acc_any(ctx, lane, P, b, offset, n, sval, bstart, job);
-  } else {
-    // infinity terms (all-zero XYZZ) of the agreed shape, and the status block
-    uint32_t* zeros = nullptr;
+  } else if (!rc) {
+    // empty shard: the status block alone ("empty", no bit sums)
+    uint32_t* buf = nullptr;
     if (!(rc = get_lane(ctx, &lane)) &&
-        !(rc = lane->ws.get("msm_zero_terms", (words + SHARD_STATUS_WORDS) * 4, (void**)&zeros))) {
-      if (hipMemsetAsync(zeros, 0, words * 4, lane->st) != hipSuccess) {
-        (void)hipGetLastError();
-        set_error("msm_sharded: hipMemsetAsync failed");
-        rc = ZKMI_EHIP;
-      } else {
-        rc = msm_queue_handover(ctx, lane, lane->st, job, zeros, words);
-      }
-    }
+        !(rc = lane->ws.get("msm_empty_shard", SHARD_PAYLOAD_WORDS * 4, (void**)&buf)))
+      rc = msm_queue_handover(ctx, lane, lane->st, job, buf, 0);
   }
   if (rc) {
-    // the peers are in (or heading for) this job's data exchange: join it with
-    // a failure status unless this rank's share is already queued (RCCL)
-    if (!job->exchanged && comm->kind == ZKMI_COMM_RCCL) {
-      const std::string err = zkmi_last_error();
-      (void)comm_fail_exchange(comm, words + SHARD_STATUS_WORDS);
-      set_error("%s", err.c_str());
-    } else if (comm->kind == ZKMI_COMM_HOST) {
-      const std::string err = zkmi_last_error();
-      (void)comm_fail_exchange(comm, words + SHARD_STATUS_WORDS);
-      set_error("%s", err.c_str());
-    }
+    // the peers are in (or heading for) this job's exchange: join it with a
+    // failure status unless this rank's share is already queued (RCCL)
+    const std::string err = zkmi_last_error();
+    if (!(job->exchanged && comm->kind == ZKMI_COMM_RCCL)) (void)comm_fail_exchange(comm, SHARD_PAYLOAD_WORDS);
+    set_error("%s", err.c_str());
     msm_job_free(job);
     return rc;
   }

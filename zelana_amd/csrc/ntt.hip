@@ -270,7 +270,7 @@ __device__ __forceinline__ Fe ntt_tab_scale(Fe v, uint64_t i, const NttIo& io) {
 // to hide the load and twiddle latency the 2-wave form exposes).
 
 template <bool DIT, int PRO, int EPI, bool PERM, int TB, int RB>
-__global__ void __launch_bounds__(256, (RB == 3 ? 2 : 4)) k_ntt_group(const uint32_t* src, uint32_t* dst,
+__global__ void __launch_bounds__(1 << (TB - RB), (RB == 3 ? 2 : 4) * 256 / (1 << (TB - RB))) k_ntt_group(const uint32_t* src, uint32_t* dst,
                                                                           const uint32_t* __restrict__ tw, uint32_t logn,
                                                                           uint32_t a, uint32_t k, NttIo io) {
   constexpr int TILE = 1 << TB, EPT = 1 << RB;
@@ -525,11 +525,31 @@ static std::vector<uint32_t> ntt_groups(uint32_t logn) {
   return ks;
 }
 
-// group kernel shape: 1024-element radix-4 tiles (4 waves/SIMD; measured 7%
-// faster than a 2048-element radix-8 form, which was dropped)
+// group kernel shape: radix-4 register rounds (4 elements per thread, <= 128
+// VGPRs: 4 waves/SIMD; a 2048-element radix-8 form was 7% slower, dropped).
+// Passes with column bits (every pass of a large transform but the innermost)
+// read 2^(TB - k) adjacent columns per row of the tile: 1024-element tiles of
+// 256 threads give 4 columns = 128-B bursts at 2^(a - k)-element strides (2 MB
+// at 2^24).  ZK_NTT_TB_OUTER = 12 runs those passes on 4096-element tiles of
+// 1024 threads (147 KB of LDS, one workgroup = 16 waves per CU, the same 4
+// waves/SIMD): 16 columns = 512-B bursts.  Measured (round 5, one box, 3
+// interleaved repeats, tools/gpu_r05e.sh): 2^24 NTT+INTT group time 4.25 ms
+// with 1024-element tiles against 5.58-5.97 ms with 4096 (2^22: 1.13 vs 1.32
+// ms) -- the 16-wave barriers of the big tile cost more than the longer bursts
+// save -- so the default stays 10.
+#ifndef ZK_NTT_TB_OUTER
+#define ZK_NTT_TB_OUTER 10
+#endif
 template <bool DIT, int PRO, int EPI, bool PERM>
 static void launch_group(hipStream_t st, const uint32_t* src, uint32_t* dst, const uint32_t* tw, uint32_t logn,
                          uint32_t a, uint32_t k, const NttIo& io) {
+  constexpr int TBo = ZK_NTT_TB_OUTER;
+  if (TBo != 10 && !PERM && a > k && logn >= (uint32_t)TBo && k <= (uint32_t)TBo - 2) {  // a pass with column bits
+    const size_t sm = ((size_t)1 << TBo) * NL * 4;
+    const unsigned grid = (unsigned)((1ull << logn) >> TBo);
+    k_ntt_group<DIT, PRO, EPI, PERM, TBo, 2><<<grid, 1 << (TBo - 2), sm, st>>>(src, dst, tw, logn, a, k, io);
+    return;
+  }
   const size_t sm = (size_t)1024 * NL * 4;
   const unsigned grid = (unsigned)((1ull << logn) / 1024);
   k_ntt_group<DIT, PRO, EPI, PERM, 10, 2><<<grid, 256, sm, st>>>(src, dst, tw, logn, a, k, io);

@@ -583,7 +583,7 @@ struct zkmi_wprog {
 namespace zk {
 static void wprog_free(zkmi_wprog* p) {
   if (!p) return;
-  if (p->st) (void)hipStreamSynchronize(p->st);
+  (void)hipStreamSynchronize(p->st ? p->st : p->ctx->stream);  // runs beside a communicator use the context stream
   (void)hipFree(p->d_input_var);
   (void)hipFree(p->d_coeff);
   (void)hipFree(p->d_rc);
@@ -599,8 +599,36 @@ static void wprog_free(zkmi_wprog* p) {
   }
   if (p->done) (void)hipEventDestroy(p->done);
   if (p->ctx_mark) (void)hipEventDestroy(p->ctx_mark);
-  if (p->st) (void)hipStreamDestroy(p->st);
+  if (p->st) {
+    (void)hipStreamDestroy(p->st);
+    p->ctx->nstreams--;
+  }
   delete p;
+}
+
+// The stream a run goes on: its own highest-priority stream (the program is a
+// chain of ~140 small launches that must get onto CUs between the blocks of
+// the proof running beside it), made at the first run -- or, while a
+// communicator exists on the context, the context stream (stream budget,
+// no fifth stream beside context + 2 lanes + the RCCL stream).
+static int wprog_stream(zkmi_ctx* ctx, zkmi_wprog* p, hipStream_t* st) {
+  if (ctx->ncomm > 0) {
+    *st = ctx->stream;
+    return 0;
+  }
+  if (!p->st) {
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipStreamCreateWithPriority(&p->st, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      (void)hipGetLastError();
+      p->st = nullptr;
+      set_error("zkmi_wprog_run: cannot create the program's stream");
+      return ZKMI_EHIP;
+    }
+    ctx->nstreams++;
+  }
+  *st = p->st;
+  return 0;
 }
 }  // namespace zk
 
@@ -685,12 +713,7 @@ int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* d, zkmi_wprog** out)
     wprog_free(p);
     return ZKMI_EHIP;
   };
-  // Highest stream priority: the program is a chain of ~140 small launches
-  // that must get onto CUs between the blocks of the proof running beside it
-  int prio_lo = 0, prio_hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipStreamCreateWithPriority(&p->st, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipEventCreateWithFlags(&p->done, hipEventDisableTiming) != hipSuccess ||
+  if (hipEventCreateWithFlags(&p->done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->ctx_mark, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->in_done[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&p->in_done[1], hipEventDisableTiming) != hipSuccess)
@@ -743,7 +766,7 @@ int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* d, zkmi_wprog** out)
   // MiMC round constants c_i = (i+1)^3 + (i+1) (poseidon.nr:15-56)
   uint64_t rc[MIMC_R * 4] = {0};
   for (int i = 0; i < MIMC_R; i++) rc[4 * i] = (uint64_t)(i + 1) * (i + 1) * (i + 1) + (i + 1);
-  hipStream_t st = p->st;
+  hipStream_t st = ctx->stream;  // the run stream is made at the first run (wprog_stream)
   if (hipMemcpyAsync(p->d_input_var, d->input_var, ni * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
       (d->num_ops && hipMemcpyAsync(p->d_ops, d->op, d->num_ops * 16, hipMemcpyHostToDevice, st) != hipSuccess) ||
       (d->num_terms && hipMemcpyAsync(p->d_terms, d->term, d->num_terms * 8, hipMemcpyHostToDevice, st) != hipSuccess) ||
@@ -771,7 +794,8 @@ int zkmi_wprog_run_many(zkmi_ctx* ctx, zkmi_wprog* p, size_t nb, const uint64_t*
     set_error("zkmi_wprog_run: bad arguments");
     return ZKMI_EINVAL;
   }
-  hipStream_t st = p->st;
+  hipStream_t st;
+  ZK_TRY(wprog_stream(ctx, p, &st));
   // The z this run writes was last read by context work enqueued before the
   // previous run (callers alternate two z buffers / buffer sets): wait for
   // exactly that, so this run overlaps the previous batches' proofs.

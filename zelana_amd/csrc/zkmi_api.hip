@@ -4,6 +4,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include <atomic>
 
 #include "zkmi_internal.h"
@@ -16,6 +18,13 @@ void set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
+}
+
+void note_cleared_error(hipError_t e, const char* fn) {
+  static std::atomic<int> seen{0};
+  if (seen.fetch_add(1) < 8)
+    fprintf(stderr, "libzkmi: %s entered with a pending HIP error (%s); cleared\n", fn ? fn : "?",
+            hipGetErrorString(e));
 }
 
 
@@ -150,6 +159,7 @@ int zkmi_ctx_create(int device, zkmi_ctx** out) {
     set_error("hipStreamCreate failed");
     return ZKMI_EHIP;
   }
+  c->nstreams = 1;
   *out = c;
   return 0;
 }
@@ -168,6 +178,7 @@ void zkmi_ctx_destroy(zkmi_ctx* ctx) {
     delete l;
   }
   ctx->lanes.clear();
+  ctx->nstreams = 1;
   if (ctx->prove_fork) hipEventDestroy(ctx->prove_fork);
   for (auto& pb : ctx->pinned_free) hipHostFree(pb.first);
   ctx->pinned_free.clear();
@@ -364,9 +375,12 @@ int zkmi_msm_set_lanes(zkmi_ctx* ctx, int lanes) {
     set_error("zkmi_msm_set_lanes: lanes must be in [1, 8]");
     return ZKMI_EINVAL;
   }
-  ctx->msm_lanes = lanes;
+  // stream budget: at most MAX_LANES_WITH_COMM lanes beside a communicator
+  ctx->msm_lanes = ctx->ncomm ? std::min(lanes, MAX_LANES_WITH_COMM) : lanes;
   return 0;
 }
+int zkmi_msm_get_lanes(const zkmi_ctx* ctx) { return ctx ? ctx->msm_lanes : -1; }
+int zkmi_ctx_stream_count(const zkmi_ctx* ctx) { return ctx ? ctx->nstreams : -1; }
 int zkmi_msm_set_window(zkmi_ctx* ctx, int c) {
   if (c != 0 && (c < 4 || c > 17)) {
     set_error("window %d outside [4, 17]", c);

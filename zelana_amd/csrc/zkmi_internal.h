@@ -47,6 +47,13 @@ struct MsmLane {
   hipEvent_t fork = nullptr, consumed = nullptr;
   hipEvent_t acc_done = nullptr;  // end of this lane's last table accumulation (msm.hip acc chain)
   int debug_sorted = 0;  // ZKMI_DEBUG_SKIP ablations only (msm.hip)
+  // bin-sort counter blocks (msm.hip BsGeom): two, alternating per sort; the
+  // one the last sort used (its accumulations read the item counters)
+  void* bs_ctr = nullptr;
+  size_t bs_ctr_words = 0;
+  int bs_parity = 0;
+  bool bs_dirty = false;  // a sort's kernels were not all queued: clear both blocks next time
+  uint32_t* bs_cur = nullptr;
 };
 
 struct KernelTimer {
@@ -80,7 +87,16 @@ struct zkmi_ctx {
   // lane) starts after it (msm.hip msm_acc_phase)
   zk::MsmLane* acc_last = nullptr;
   hipEvent_t prove_fork = nullptr;  // owned: the event groth16_prove_submit uses for it
+  // Stream budget: communicators alive on this context, and the
+  // streams the library holds for it (context, lanes, communicators', witness
+  // programs').  While a communicator exists the lanes are capped at
+  // MAX_LANES_WITH_COMM and witness programs run on the context stream, so the
+  // process holds <= GPU_MAX_HW_QUEUES (4) streams and the RCCL stream never
+  // shares a hardware queue with MSM work.
+  int ncomm = 0;
+  int nstreams = 0;
 };
+constexpr int MAX_LANES_WITH_COMM = 2;
 
 struct zkmi_bases {
   zkmi_ctx* ctx;
@@ -96,16 +112,6 @@ struct zkmi_bases {
   // 1: full table (tw = 1) with balanced window widths -- copy j is
   // 2^(offset of window j) * P_i, WinLayout<tc, true> in msm.hip
   int tbal = 0;
-  // Window plans agreed with the other ranks of a communicator for this shard
-  // (msm_submit_sharded): the first sharded MSM of a (communicator, n, table
-  // state, window setting) runs the header all-gather, later ones reuse it.
-  struct AgreedPlan {
-    uint64_t comm_serial;
-    size_t n;
-    int window, tc, tp, tw, tbal;
-    uint32_t hdr[4];  // agreed c, W, bb, sb (c = 0: every shard empty)
-  };
-  mutable std::vector<AgreedPlan> agreed;
 };
 
 // Multi-rank communicator (zkmi.h multi-GPU section; comm.hip).
@@ -113,19 +119,15 @@ constexpr int ZKMI_COMM_RCCL = 0;
 constexpr int ZKMI_COMM_HOST = 1;
 struct zkmi_comm {
   zkmi_ctx* ctx = nullptr;
-  uint64_t serial = 0;                  // process-unique (keys zkmi_bases::agreed)
+  uint64_t serial = 0;                  // process-unique
   int nranks = 1, rank = 0, kind = ZKMI_COMM_RCCL;
-  void* nccl = nullptr;                 // ncclComm_t (RCCL transport): bit-sum exchanges
-  void* nccl_ctl = nullptr;             // split of it for the synchronous plan headers
-  hipStream_t st = nullptr;             // every bit-sum exchange, in issue order
-  hipStream_t st_ctl = nullptr;         // header exchanges (never wait behind queued MSMs)
+  void* nccl = nullptr;                 // ncclComm_t (RCCL transport): the sharded-MSM exchanges
+  hipStream_t st = nullptr;             // every exchange, in issue order (the process's only RCCL stream)
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
-  uint32_t* d_stage = nullptr;          // device staging for host-buffer collectives
-  size_t stage_bytes = 0;
   zkmi_allgather_fn fn = nullptr;       // host transport
   void* user = nullptr;
-  // RCCL: device buffer (nranks x fail_words) for the failure exchange of a
-  // sharded MSM that fails after its plan was agreed (comm_fail_exchange)
+  // RCCL: device buffer (fail_words = nranks x one payload) for the failure
+  // exchange of a rank whose sharded MSM fails before its exchange is queued
   uint32_t* d_fail = nullptr;
   size_t fail_words = 0;
 };
@@ -135,16 +137,16 @@ namespace zk {
 // already queued on `lane_st` and before anything queued there afterwards
 // (RCCL transport only).
 int comm_allgather_device(zkmi_comm* c, hipStream_t lane_st, const void* d_send, void* d_recv, size_t bytes);
-// Synchronous all-gather of host buffers (either transport).
+// Synchronous all-gather of host buffers (host transport only).
 int comm_allgather_host(zkmi_comm* c, const void* send, void* recv, size_t bytes);
 int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
                        zkmi_msm_job** out);
-// A rank whose sharded MSM fails after the plan exchange still takes part in
-// the job's data exchange (`words` u32 per rank, the last 4 a status block),
-// with its status word set, so the other ranks fail in their msm_wait instead
+// A rank whose sharded MSM fails before its exchange is queued still takes
+// part in the job's exchange (`words` u32 per rank, a status block first),
+// with its failure flag set, so the other ranks fail in their msm_wait instead
 // of blocking in the collective.  Synchronous; issue order as the exchange.
 int comm_fail_exchange(zkmi_comm* c, size_t words);
-// words of the status block that ends every rank's sharded exchange payload
+// words of the status block that starts every rank's sharded exchange payload
 constexpr size_t SHARD_STATUS_WORDS = 4;
 
 // HIP's current device is per host thread (default 0).  Every entry point that
@@ -152,6 +154,10 @@ constexpr size_t SHARD_STATUS_WORDS = 4;
 // duration of the call and restores the caller's device on return, so a
 // context made for device k can be driven from any thread (e.g. a tokio
 // blocking-pool thread) without touching GPU 0.
+// a pending HIP error cleared on entry (DeviceGuard): reported on stderr (the
+// first few per process), so a fault left by an earlier unchecked call is
+// never lost silently
+void note_cleared_error(hipError_t e, const char* fn);
 struct DeviceGuard {
   int prev = -1;
   bool restore = false;
@@ -160,8 +166,8 @@ struct DeviceGuard {
     // state must not be reported by this call's first hipGetLastError
     // (seen: "invalid device ordinal" left in the test process between two
     // contexts' lifetimes, then reported by zkmi_pk_load's launch check)
-    (void)fn;
-    (void)hipGetLastError();
+    const hipError_t pending = hipGetLastError();
+    if (pending != hipSuccess) note_cleared_error(pending, fn);
     if (dev < 0) return;
     if (hipGetDevice(&prev) != hipSuccess) {
       (void)hipGetLastError();

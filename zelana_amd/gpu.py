@@ -140,12 +140,17 @@ class Context:
         check(lib().zkmi_msm_set_window(self.h, c))
 
     def set_lanes(self, lanes: int):
+        """MSM lanes (capped at 2 while a communicator exists: stream budget)."""
         check(lib().zkmi_msm_set_lanes(self.h, lanes))
-        self._lanes = lanes
 
     def lanes(self) -> int:
-        """MSM lanes last set through set_lanes (the context's default is 2)."""
-        return getattr(self, "_lanes", 2)
+        """MSM lanes in effect."""
+        return lib().zkmi_msm_get_lanes(self.h)
+
+    def stream_count(self) -> int:
+        """Streams the library holds for this context (context, lanes,
+        communicator and witness-program streams)."""
+        return lib().zkmi_ctx_stream_count(self.h)
 
     def sync(self):
         check(lib().zkmi_sync(self.h))
