@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--l2-log-n", type=int, default=22, help="Groth16 domain 2^k for the L2 proof measurement")
     ap.add_argument("--l2-steps", type=int, default=8)
     ap.add_argument("--no-zbatch", action="store_true", help="skip the zelana_batch (batch 70) proof measurement")
+    ap.add_argument("--no-g2", action="store_true", help="skip the 2^20 G2 MSM side measurement")
     ap.add_argument("--no-big", action="store_true", help="skip the config-5 global 2^26 MSM (sharded over all ranks)")
     ap.add_argument("--big-log-n", type=int, default=26, help="global MSM size 2^k of the config-5 measurement")
     ap.add_argument("--big-steps", type=int, default=5)
@@ -74,6 +75,7 @@ def parse():
     return ap.parse_args()
 
 
+R_FR = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 _T0 = time.perf_counter()
 
 
@@ -159,10 +161,11 @@ def main():
         return out
 
     ctx.set_lanes(args.lanes)
+    lanes = ctx.lanes()  # capped at 2 beside a communicator (stream budget)
 
     def run(k):
-        """k MSM steps, pipelined: args.lanes MSMs in flight, one per lane."""
-        return pipelined(lambda: submit(bases, scalars, n), finish, k, args.depth or args.lanes)
+        """k MSM steps, pipelined: one MSM in flight per lane."""
+        return pipelined(lambda: submit(bases, scalars, n), finish, k, args.depth or lanes)
 
     def timed(k, warm, prof=False):
         """prof: HIP-event stage timers on (the stage breakdown comes from a
@@ -195,7 +198,7 @@ def main():
         # warm every lane (first use of a lane allocates its workspace: a
         # 1-step warmup left two of three lanes' hipMallocs in the timed region,
         # which is what swung this number between runs: 240-306 Mpt/s)
-        pres, pdt = timed(psteps, 2 * args.lanes)
+        pres, pdt = timed(psteps, 2 * lanes)
         timed(psteps, 0, prof=True)
         plain = {"value": round(n * world * psteps / pdt / 1e6, 2), "ms_per_step": round(pdt / psteps * 1e3, 4),
                  "stage_ms_per_step": stages(psteps)}
@@ -226,17 +229,17 @@ def main():
         ctx.msm(bases, scalars)
     ktot, kcnt = ctx.profile_get(kernel)
     ctx.profile(False)
-    ctx.set_lanes(args.lanes)
+    ctx.set_lanes(lanes)
     kavg_s = ktot / max(kcnt, 1) / 1e3
     achieved = MSM_BYTES_PER_PAIR * n / kavg_s / 1e9 if kcnt else None
     # acc0_g1 launches before the roofline pass (for tools/rocpd_summary.py)
-    rf_first = ((0 if args.no_plain else 2 * args.lanes + 2 * max(1, args.steps // 2)) + args.warmup
+    rf_first = ((0 if args.no_plain else 2 * lanes + 2 * max(1, args.steps // 2)) + args.warmup
                 + args.steps * (1 if args.timers_in_timed_region else 2))
     pairs_total = n * world * args.steps
     value = pairs_total / elapsed / 1e6
 
     extra = {"msm_stage_ms_per_step": breakdown, "fixed_base_table": table, "msm_plain_no_table": plain,
-             "lanes": args.lanes}
+             "lanes": lanes}
     if comm is not None:
         extra["msm_exchange"] = {"transport": ("rccl" if comm.info()[2] == 0 else "host:" + backend),
                                  "what": "all-gather of every rank's per-window bit sums inside libzkmi "
@@ -252,7 +255,11 @@ def main():
             allgather, big_state)
         if comm is not None:
             extra["msm_exchange"]["per_rank"] = extra["msm_global_2_%d" % args.big_log_n].get("per_rank")
-    ntt_state = zb_state = None
+    if not args.no_g2:
+        log("G2 MSM 2^%d" % args.log_n)
+        extra["msm_g2_2_%d" % args.log_n] = bench_msm_g2(ctx, args.log_n, max(4, args.steps // 2), rank, world,
+                                                         sync_all, allmax)
+    ntt_state = zb_state = l2_state = None
     if args.no_big:
         big_state = None
     if not args.no_ntt:
@@ -260,7 +267,8 @@ def main():
         extra["ntt"], ntt_state = bench_ntt(ctx, args.ntt_log_n, world, sync_all, allmax)
     if not args.no_l2:
         log("L2-scale proofs")
-        extra["l2_proofs"] = bench_l2(ctx, args.l2_log_n, args.l2_steps, rank, world, sync_all, allmax)
+        l2_state = {} if (rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_cpu_prove) else None
+        extra["l2_proofs"] = bench_l2(ctx, args.l2_log_n, args.l2_steps, rank, world, sync_all, allmax, l2_state)
     if not args.no_zbatch:
         log("zelana_batch proofs")
         extra["zelana_batch_proofs"], zb_state = bench_zbatch(ctx, args.l2_steps, world, sync_all, allmax)
@@ -272,7 +280,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("CPU baseline legs")
         cpu = cpu_baseline(ctx, bases, scalars, n, result, args.cpu_threads, ntt_state,
-                           None if args.no_cpu_prove else zb_state, c1_state, big_state)
+                           None if args.no_cpu_prove else zb_state, c1_state, big_state, l2_state)
+        if "l2_2_22" in cpu["legs"] and "l2_proofs" in extra:
+            extra["l2_proofs"]["proof_equal_oracle"] = cpu["legs"]["l2_2_22"]["gpu_matches_cpu"]
 
     pmc = pmc_record(kernel, args.log_n)
     traffic = pmc.get("hbm_bytes")
@@ -313,6 +323,10 @@ def main():
                         + ("; fixed-base table built once per base set (as for a proving key), outside the timed region"
                            if table else ""),
             "log_n_per_gpu": args.log_n,
+            "table": ({"window": table["window"], "copies": table["copies"], "build_s": table["build_s"],
+                       "what": "fixed-base table of the bases (a proving key's are fixed), built outside the timed "
+                               "region; the plain-Pippenger figure is extra.msm_plain_no_table"}
+                      if table else None),
             "parallelism": f"point-shard x{world} + RCCL all-gather of partials" if world > 1 else "single GPU",
             "field": "BN254 Fq, 9x29-bit limbs, Montgomery R=2^261",
             "env": env_knobs,
@@ -330,7 +344,7 @@ def main():
             "kernel_avg_ms_in_timed_region": round(ovl_tot / max(ovl_cnt, 1), 4),
             "algorithmic_bytes_per_launch": MSM_BYTES_PER_PAIR * n,
             "note": "MSM is VALU-bound (256-bit modular multiplies), not HBM-bound; frac is vs HBM peak as BASELINE.md "
-                    "defines. kernel_avg_ms = isolated launches (one lane); the timed region runs " + str(args.lanes) + " lanes whose "
+                    "defines. kernel_avg_ms = isolated launches (one lane); the timed region runs " + str(lanes) + " lanes whose "
                     "kernels overlap",
         },
         "valu_roofline": valu,
@@ -461,6 +475,58 @@ def bench_msm_sharded(ctx, log_total, steps, world, rank, submit, finish, sync_a
     }
 
 
+def bench_msm_g2(ctx, log_n, steps, rank, world, sync_all, allmax, lanes=2):
+    """BN254 G2 MSM at the headline's size: b_g2_query's MSM in every proof
+    (core/src/sequencer/settlement/prover.rs:408 -> ark-groth16's b_g2 MSM,
+    SURVEY.md §8a a8).  2^log_n uniform scalars (StdRng(40 + rank)) over G2
+    points generated in HBM, with the fixed-base table a proving key gets (and
+    the plain pass before it), lanes MSMs in flight; per-GPU work, so the
+    aggregate is weak-scaling like the headline."""
+    from zelana_amd.host_prover import stdrng_fr
+
+    n = 1 << log_n
+    bases = ctx.bases_generate(seed=2040 + rank, n=n, g2=True)
+    sc = ctx.scalars_upload(stdrng_fr(40 + rank, n))
+    prev_lanes = ctx.lanes()
+    ctx.set_lanes(lanes)
+
+    def timed(k):
+        pipelined(lambda: ctx.msm_submit(bases, sc, n), ctx.msm_wait, 2 * lanes, lanes)  # lanes warm
+        sync_all()
+        t0 = time.perf_counter()
+        res = pipelined(lambda: ctx.msm_submit(bases, sc, n), ctx.msm_wait, k, lanes)
+        sync_all()
+        return res, allmax(time.perf_counter() - t0)
+
+    plain_res, plain_dt = timed(max(2, steps // 2))
+    t0 = time.perf_counter()
+    info = bases.precompute()
+    table_s = time.perf_counter() - t0
+    res, dt = timed(steps)
+    ctx.profile(True)
+    ctx.profile_reset()
+    ctx.set_lanes(1)
+    for _ in range(3):  # isolated accumulation time (one lane)
+        ctx.msm(bases, sc)
+    acc_t, acc_c = ctx.profile_get("msm_acc0_g2")
+    ctx.profile(False)
+    ctx.set_lanes(prev_lanes)
+    del bases, sc
+    return {
+        "workload": f"BN254 G2 MSM, 2^{log_n} uniform scalars per GPU over G2 points in HBM (b_g2_query's MSM, "
+                    f"SURVEY.md §8a a8); {lanes} lanes",
+        "value": round(n * world * steps / dt / 1e6, 2),
+        "unit": "Mpoint-scalar/s",
+        "ms_per_msm": round(dt / steps * 1e3, 3),
+        "steps": steps,
+        "table": {"window": info[1], "copies": info[2], "build_s": round(table_s, 2)},
+        "plain_no_table": {"value": round(n * world * max(2, steps // 2) / plain_dt / 1e6, 2),
+                           "ms_per_msm": round(plain_dt / max(2, steps // 2) * 1e3, 3)},
+        "same_result_plain_and_table": bool(np.array_equal(res, plain_res)),
+        "acc_g2_isolated_ms": round(acc_t / max(acc_c, 1), 3) if acc_c else None,
+    }
+
+
 def bench_ntt(ctx, log_n, world, sync_all, allmax, steps=5):
     """Forward + inverse NTT of length 2^log_n on device data (configs[2]);
     replicas at N > 1 (the transform does not shard).
@@ -513,27 +579,43 @@ def bench_ntt(ctx, log_n, world, sync_all, allmax, steps=5):
     return line, {"log_n": log_n, "x": x0, "fwd": fwd}
 
 
-def bench_l2(ctx, log_n, steps, rank, world, sync_all, allmax):
+def bench_l2(ctx, log_n, steps, rank, world, sync_all, allmax, keep=None):
     """Groth16 proofs/s at the config-4 scale (BASELINE.json configs[3]:
-    ~2^22-constraint L2 block proof): synthetic R1CS of 2^log_n - 8 rows
-    (3 terms per row in A and B, 1 in C; 8 instance variables = One + 7
-    public inputs; one witness per row), random proving key of that shape
-    generated in HBM, witness resident in HBM.  One step = witness map
-    (3 mat-vecs, 7 NTTs) + 4 G1 MSMs + 1 G2 MSM + assembly.  At N > 1 every
-    rank proves its own batches (replicas)."""
-    from zelana_amd import gpu
-    from zelana_amd.r1cs import synthetic_fast
+    ~2^22-constraint L2 block proof) under a REAL key: the satisfiable
+    synthetic circuit wprog.synthetic_program (2^log_n - 8 constraints, 3
+    terms per row in A and B over the free variables and earlier layers'
+    products, C = the row's product variable, 4 layers; 8 instance variables
+    = One + 7 public inputs), its Groth16 key from circuit_specific_setup on
+    the GPU (StdRng(70 + rank)), z written in HBM by the circuit's witness
+    program.  One step = witness map (3 mat-vecs, 7 NTTs) + 4 G1 MSMs + 1 G2
+    MSM + assembly from the resident z.  The first proof is checked by the
+    product's verifier (zkmi_groth16_verify) and, on rank 0 at N = 1, equals
+    the CPU oracle's proof under the oracle's own setup (cpu_baseline leg
+    l2_2_22).  At N > 1 every rank proves its own batches (replicas)."""
+    from zelana_amd import gpu, wprog as W
+    from zelana_amd.keygen import circuit_specific_setup
+    from zelana_amd.rng import StdRng
 
     l = 8
     m = (1 << log_n) - l
-    w = m
+    w_in = 1 << (log_n - 6)
+    seed = 70 + rank
     t0 = time.perf_counter()
-    cs, z = synthetic_fast(m, l, w, seed=70 + rank)
-    pk = gpu.synthetic_pk(ctx, 70 + rank, log_n, l, w)
+    cs, prog, inputs = W.synthetic_program(m, l, w_in, seed=seed)
+    build_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    pk, vk = circuit_specific_setup(ctx, cs, StdRng.seed_from_u64(seed))
+    ctx.sync()
+    keygen_s = time.perf_counter() - t0
     dev = gpu.R1CSDevice(ctx, cs)
-    dz = gpu.DeviceBuffer(ctx, z.nbytes)
-    dz.upload(z)
-    setup_s = time.perf_counter() - t0
+    wp = W.WitnessProgram(ctx, prog)
+    dz = gpu.DeviceBuffer(ctx, prog.num_vars * 32)
+    wp.run(inputs, dz)
+    t0 = time.perf_counter()
+    wp.run(inputs, dz)
+    witness_ms = (time.perf_counter() - t0) * 1e3
+    z = None
+    setup_s = build_s + keygen_s
 
     def timed():
         # one warm proof per lane: a proof's 5 MSMs rotate over the lanes, so
@@ -585,12 +667,27 @@ def bench_l2(ctx, log_n, steps, rank, world, sync_all, allmax):
     pdt = allmax((time.perf_counter() - t0) / steps)
     pipe_same = all(all(np.array_equal(x, y) for x, y in zip(o1, o2)) for o1, o2 in zip(pouts, outs))
     nnz = int(sum(cs.csr(k)[0][-1] for k in ("a", "b", "c")))
-    del dev, pk
+    pub = [sum(int(inputs[i, k]) << (64 * k) for k in range(4)) for i in range(1, l)]
+    verifies = gpu.groth16_verify(vk, pub, *outs[0])
+    pub[0] = (pub[0] + 1) % R_FR
+    rejects_changed_input = not gpu.groth16_verify(vk, pub, *outs[0])
+    if keep is not None and world == 1:  # the CPU leg proves the same z, r, s under the oracle's setup
+        z = np.zeros((prog.num_vars, 4), np.uint64)
+        dz.download(z)
+        keep.update(cs=cs, z=z, seed=seed, r=12345, s=67890, proof=outs[0])
+    wp.close()
+    del dev, pk, dz
     return {
-        "workload": f"Groth16 prove, domain 2^{log_n}: {m} constraints, {l} instance + {w} witness vars, {nnz} non-zeros "
-                    "(BASELINE.json configs[3] scale; synthetic R1CS + random pk generated in HBM; the reference's "
-                    "own L2BlockCircuit R1CS is parity-unpinned: no reference fixture covers it)"
+        "workload": f"Groth16 prove, domain 2^{log_n}: {m} constraints, {l} instance + {prog.num_vars - l} witness vars, "
+                    f"{nnz} non-zeros (BASELINE.json configs[3] scale; satisfiable synthetic circuit "
+                    "wprog.synthetic_program, real key from GPU circuit_specific_setup(StdRng(70 + rank)); the "
+                    "reference's own L2BlockCircuit R1CS is parity-unpinned: no reference fixture covers it)"
                     + (f"; {world} replicas, one per GPU" if world > 1 else ""),
+        "verifies": bool(verifies),
+        "rejects_changed_public_input": bool(rejects_changed_input),
+        "proof_equal_oracle": None,  # filled by cpu_baseline's l2_2_22 leg (rank 0, N = 1)
+        "keygen_s": round(keygen_s, 2),
+        "witness_program_ms": round(witness_ms, 2),
         "proofs_per_s": round(world / dt, 3),
         "proofs_per_s_per_gpu": round(1.0 / dt, 3),
         "ms_per_proof": round(dt * 1e3, 2),
@@ -603,7 +700,8 @@ def bench_l2(ctx, log_n, steps, rank, world, sync_all, allmax):
         "plain_no_table": {"proofs_per_s": round(world / plain_dt, 3), "ms_per_proof": round(plain_dt * 1e3, 2),
                            "stage_ms_per_proof": plain_st},
         "setup_s": round(setup_s, 1),
-        "note": "witness z resident in HBM; uploading it costs z_bytes/PCIe extra (see DESIGN.md)",
+        "note": "witness z resident in HBM (written there by the witness program); uploading a host z instead costs "
+                "z_bytes/PCIe extra (see DESIGN.md)",
     }
 
 
@@ -922,7 +1020,7 @@ def host_cores():
 
 
 def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb_state=None, c1_state=None,
-                 big_state=None):
+                 big_state=None, l2_state=None):
     """oracle/ restatement of arkworks on this box's host cores, same inputs
     as the GPU legs, each leg checked for equality with the GPU output:
       msm   ark-ec msm_bigint_wnaf on the headline's 2^20 bases / scalars
@@ -1031,6 +1129,33 @@ def cpu_baseline(ctx, bases, scalars, n, gpu_result, threads, ntt_state=None, zb
                                     and np.array_equal(c, gc)),
         }
         del keep, keep0, orng
+    if l2_state:
+        log("CPU config-4 leg: oracle setup + prove at 2^22")
+        cs, z = l2_state["cs"], l2_state["z"]
+        st, keep = O.make_r1cs(cs)
+        orng = O.Rng(l2_state["seed"])
+        t0 = time.perf_counter()
+        opk = O.lib().oracle_groth16_setup(ctypes.byref(st), orng.h, threads)
+        setup_s = time.perf_counter() - t0
+        a, b, c = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+        rs = np.concatenate([O.int_to_limbs(l2_state["r"]), O.int_to_limbs(l2_state["s"])])
+        t0 = time.perf_counter()
+        rc = O.lib().oracle_groth16_prove(opk, ctypes.byref(st), O.P(z), None, O.P(rs), threads,
+                                          O.P(a), O.P(b), O.P(c), None)
+        dtp = time.perf_counter() - t0
+        O.lib().oracle_pk_free(opk)
+        ga, gb, gc = l2_state["proof"]
+        out["legs"]["l2_2_22"] = {
+            "value": round(1.0 / dtp, 4), "unit": "proofs/s", "s_per_proof": round(dtp, 2), "cores": threads,
+            "kind": "port",
+            "sample": f"one Groth16 proof of extra.l2_proofs' circuit ({cs.num_constraints} constraints, 2^22 domain) "
+                      f"under the oracle's own setup from the same StdRng({l2_state['seed']}) (setup {setup_s:.1f} s, "
+                      "untimed), same z, r, s",
+            "gpu_matches_cpu": bool(rc == 0 and np.array_equal(a, ga) and np.array_equal(b, gb)
+                                    and np.array_equal(c, gc)),
+        }
+        del keep, orng
+        l2_state.clear()
     if big_state:
         log("CPU 2^%d MSM leg" % big_state["log_n"])
         pts, sc = big_state["pts"], big_state["sc"]

@@ -185,3 +185,54 @@ def _vk_points(vk: bytes, num_instance: int):
     assert int.from_bytes(vk[224:232], "little") == num_instance
     return {"alpha": g1(0), "beta": g2(32), "gamma": g2(96), "delta": g2(160),
             "ic": [g1(232 + 32 * i) for i in range(num_instance)]}
+
+
+def test_l2_2pow22_real_key_proof_matches_oracle(ctx):
+    """Config 4 at its named scale (BASELINE.json configs[3]: ~2^22
+    constraints) under a real key: bench.py's L2 leg circuit
+    (wprog.synthetic_program: 2^22 - 8 satisfiable constraints, 4 layers of
+    products), GPU keygen with StdRng(70), z written in HBM by the circuit's
+    witness program.  The GPU proof (resident, r and s from StdRng(7)) equals
+    oracle_groth16_prove under the oracle's own setup from the same seed, and
+    the product's verifier accepts it with the public inputs (and rejects a
+    changed one)."""
+    import time
+    from zelana_amd import gpu, wprog as W
+    from zelana_amd.keygen import circuit_specific_setup
+    from zelana_amd.rng import StdRng
+    t0 = time.time()
+
+    def step(what):
+        print(f"[{time.time() - t0:7.1f} s] {what}", flush=True)
+
+    cs, prog, inputs = W.synthetic_program((1 << 22) - 8, 8, 1 << 16, seed=70)
+    step("circuit built")
+    pk, vk = circuit_specific_setup(ctx, cs, StdRng.seed_from_u64(70))
+    wp = W.WitnessProgram(ctx, prog)
+    dz = gpu.DeviceBuffer(ctx, prog.num_vars * 32)
+    wp.run(inputs, dz)
+    dev = gpu.R1CSDevice(ctx, cs)
+    rng = StdRng.seed_from_u64(7)
+    r, s = rng.fr_rand(), rng.fr_rand()
+    a, b, c = gpu.groth16_prove_resident(ctx, pk, dev, dz, r, s)
+    step("GPU keygen + witness program + proof")
+    pub = [O.limbs_to_int(inputs[i]) for i in range(1, cs.num_instance)]
+    assert gpu.groth16_verify(vk, pub, a, b, c)
+    pub[3] = (pub[3] + 1) % O.R
+    assert not gpu.groth16_verify(vk, pub, a, b, c)
+    z = np.zeros((prog.num_vars, 4), np.uint64)
+    dz.download(z)
+    wp.close()
+    del dz, dev, pk
+    st, keep = O.make_r1cs(cs)
+    assert O.lib().oracle_r1cs_check(ctypes.byref(st), O.P(z)) == -1
+    orng = O.Rng(70)
+    opk = O.lib().oracle_groth16_setup(ctypes.byref(st), orng.h, _threads())
+    step("oracle setup (%d threads)" % _threads())
+    oa, ob, oc = np.zeros(8, np.uint64), np.zeros(16, np.uint64), np.zeros(8, np.uint64)
+    rs = np.concatenate([O.int_to_limbs(r), O.int_to_limbs(s)])
+    assert O.lib().oracle_groth16_prove(opk, ctypes.byref(st), O.P(z), None, O.P(rs), _threads(),
+                                        O.P(oa), O.P(ob), O.P(oc), None) == 0
+    O.lib().oracle_pk_free(opk)
+    step("oracle prove")
+    assert np.array_equal(a, oa) and np.array_equal(b, ob) and np.array_equal(c, oc), "GPU proof != oracle proof"

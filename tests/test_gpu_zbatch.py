@@ -205,6 +205,7 @@ def test_batch_worker_generate_batch_proof(ctx):
     assert res.proof == res.proof_bytes.hex() and len(res.proof_bytes) == 256
     pub = [int(h, 16) for h in res.public_inputs]
     assert pub == [O.limbs_to_int(z[i]) for i in range(1, cs.num_instance)]
+    assert pub == BW.public_values(d)  # the batch's own public values, main.nr's order
     assert len(res.public_witness_bytes) == 12 + 32 * 7
     assert PR.verify_with_oracle_vk(opk, cs.num_instance, pub, *want)
     w.close()

@@ -6,7 +6,7 @@ a batch's Prover.toml-shaped values go in, a `ProofResult` comes out with
 
   proof                 hex of proof_bytes                       (:559)
   proof_bytes           the proof                                (:560)
-  public_witness_bytes  the circuit's public inputs in the layout `parse_public_witness`
+  public_witness_bytes  the proof's public inputs (z slots 1..7 of the GPU witness) in the layout `parse_public_witness`
                         reads (:575-596): a 4-byte big-endian count, 8 more header
                         bytes, then 32 bytes per input                 (:561)
   public_inputs         parse_public_witness(public_witness_bytes): "0x" + hex of
@@ -104,7 +104,12 @@ class ZBatchProver:
         r, s = rng.fr_rand(), rng.fr_rand()
         a, b, c = gpu.groth16_prove_resident(self.ctx, self.pk, self.dev, self.dz, r, s)
         proof_bytes = gpu.proof_to_solana_bytes(a, b, c)
-        pw = public_witness_bytes(public_values(batch))
+        # the public inputs the proof binds: z slots 1..num_instance of the
+        # witness the GPU proved (not the batch dict, which a caller could
+        # pass inconsistently)
+        zp = np.zeros((self.num_instance, 4), np.uint64)
+        self.dz.download(zp)
+        pw = public_witness_bytes([sum(int(zp[i, k]) << (64 * k) for k in range(4)) for i in range(1, self.num_instance)])
         return ProofResult(proof=proof_bytes.hex(), proof_bytes=proof_bytes, public_witness_bytes=pw,
                            public_inputs=parse_public_witness(pw))
 

@@ -209,3 +209,75 @@ class WitnessProgram:
             self.close()
         except Exception:
             pass
+
+
+class ProgramArrays:
+    """A witness program given directly as arrays (the layout Plan produces):
+    what WitnessProgram needs, without a recording Builder."""
+
+    def __init__(self, num_vars, num_instance, input_var, op, term, coeff, level_start):
+        self.num_vars, self.num_instance = int(num_vars), int(num_instance)
+        self.input_var = np.ascontiguousarray(input_var, np.uint32)
+        self.op = np.ascontiguousarray(op, np.uint32)
+        self.term = np.ascontiguousarray(term, np.uint32).reshape(-1, 2)
+        self.coeff = np.ascontiguousarray(coeff, np.uint64).reshape(-1, 4)
+        self.level_start = np.ascontiguousarray(level_start, np.uint32)
+        self.num_levels = self.level_start.size - 1
+        self.kinds = self.op[:, 0] & 0xFF
+
+
+def synthetic_program(num_constraints: int, num_instance: int, num_inputs: int, layers: int = 4, terms: int = 3,
+                      pool: int = 1024, seed: int = 1):
+    """A satisfiable R1CS of Groth16-benchmark scale and its witness program
+    (BASELINE.json configs[3] at 2^22 constraints with a real key: its proofs
+    verify).  Variables: z[0] = 1, num_instance - 1 public inputs and
+    num_inputs free witnesses (all program inputs), then one product variable
+    per constraint.  Row i of layer k: A_i and B_i are `terms` random
+    (variable, coefficient) pairs over the free variables and the products of
+    layers < k, C_i = p_i, so A_i z * B_i z = z[p_i] holds by construction and
+    the program is one MUL per row, `layers` dependent levels.  Coefficients
+    come from a pool of `pool` random field elements (a real circuit's
+    coefficient set is small too).  Products of the last layer are read by no
+    row, like the half of zelana_batch's variables no B row reads.
+    Returns (cs, program, inputs) with inputs (num_instance + num_inputs, 4)
+    canonical limbs (inputs[0] = 1)."""
+    from .r1cs import R1CS, _rand_fr_array
+
+    rng = np.random.default_rng(seed)
+    m, l = num_constraints, num_instance
+    nfree = l + num_inputs
+    nv = nfree + m
+    assert nv < 2**32
+    coeff = _rand_fr_array(rng, pool)
+    coeff[0] = [1, 0, 0, 0]
+    bounds = (np.arange(layers + 1, dtype=np.int64) * m) // layers
+    acol = np.empty((m, terms), np.uint64)
+    bcol = np.empty((m, terms), np.uint64)
+    for k in range(layers):
+        r0, r1 = int(bounds[k]), int(bounds[k + 1])
+        hi = nfree + r0  # the free variables and every product of the earlier layers
+        acol[r0:r1] = rng.integers(0, hi, size=(r1 - r0, terms), dtype=np.uint64)
+        bcol[r0:r1] = rng.integers(0, hi, size=(r1 - r0, terms), dtype=np.uint64)
+    aci = rng.integers(1, pool, size=(m, terms), dtype=np.int64)
+    bci = rng.integers(1, pool, size=(m, terms), dtype=np.int64)
+    cs = R1CS(l, num_inputs + m)
+    rp = np.arange(0, (m + 1) * terms, terms, dtype=np.uint64)
+    cs.set_csr("a", rp, acol.reshape(-1), coeff[aci.reshape(-1)])
+    cs.set_csr("b", rp, bcol.reshape(-1), coeff[bci.reshape(-1)])
+    cs.set_csr("c", np.arange(m + 1, dtype=np.uint64), np.arange(nfree, nv, dtype=np.uint64),
+               np.tile(coeff[0], (m, 1)))
+    cs._m = m
+    op = np.zeros((m, 4), np.uint32)
+    op[:, 0] = KINDS["mul"] | (terms << 8) | (terms << 20)
+    op[:, 1] = np.arange(nfree, nv, dtype=np.uint32)
+    op[:, 2] = np.arange(m, dtype=np.uint32) * (2 * terms)
+    op[:, 3] = op[:, 2] + terms
+    term = np.empty((m, 2 * terms, 2), np.uint32)
+    term[:, :terms, 0] = acol
+    term[:, :terms, 1] = aci
+    term[:, terms:, 0] = bcol
+    term[:, terms:, 1] = bci
+    prog = ProgramArrays(nv, l, np.arange(nfree, dtype=np.uint32), op, term, coeff, bounds)
+    inputs = _rand_fr_array(rng, nfree)
+    inputs[0] = [1, 0, 0, 0]
+    return cs, prog, inputs
