@@ -25,7 +25,9 @@ ARCH = os.environ.get("ZKMI_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
              "-Wno-unused-variable", "-Wno-unused-but-set-variable"] + os.environ.get("ZKMI_HIPFLAGS", "").split()
-CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+# BMI2 / ADX: flag-free 64-bit multiplies for the host field (Fq CIOS product
+# ~50 -> ~35 ns here); every x86-64 host of an MI355X node has them
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-mbmi2", "-madx"]
 
 
 def _headers():

@@ -850,6 +850,7 @@ struct zkmi_proof_job {
   const zkmi_pk* pk;
   zkmi_msm_job* jobs[5];  // h, l, a, b_g1, b_g2
   uint64_t r[4], s[4];
+  zk::G16Asm asm_st;  // the staged assembly (msm_host.cpp)
 };
 
 namespace zk {
@@ -956,6 +957,8 @@ int groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, co
     delete pj;
     return rc;
   }
+  // the key-only part of the assembly (r delta_1, s delta_2) while the GPU works
+  groth16_asm_fixed(pk->delta_g1, pk->delta_g2, pj->r, pj->s, &pj->asm_st);
   *out = pj;
   return 0;
 }
@@ -964,17 +967,23 @@ int groth16_prove_wait(zkmi_proof_job* pj, uint64_t a_out[8], uint64_t b_out[16]
   const zkmi_pk* pk = pj->pk;
   zkmi_msm_job** jobs = pj->jobs;
   uint64_t h_acc[8], l_acc[8], a_acc[8], b1_acc[8], b2_acc[16];
+  uint64_t b_tmp[16];
   int rc = 0;
+  // each assembly stage runs as soon as its MSMs are in, beside the GPU's
+  // remaining work (the h MSM, after the witness map, ends last)
   if (!rc) rc = msm_wait(jobs[1], l_acc), jobs[1] = nullptr;
   if (!rc) rc = msm_wait(jobs[2], a_acc), jobs[2] = nullptr;
   if (!rc) rc = msm_wait(jobs[3], b1_acc), jobs[3] = nullptr;
+  if (!rc) groth16_asm_ab(pk->alpha_g1, pk->beta_g1, pk->a0, pk->b1_0, a_acc, b1_acc, pj->r, pj->s, &pj->asm_st);
   if (!rc) rc = msm_wait(jobs[4], b2_acc), jobs[4] = nullptr;
+  if (!rc) groth16_asm_b(pk->beta_g2, pk->b2_0, b2_acc, &pj->asm_st, b_tmp);
   if (!rc) rc = msm_wait(jobs[0], h_acc), jobs[0] = nullptr;
   for (int i = 0; i < 5; i++)
     if (jobs[i]) msm_job_free(jobs[i]);
-  if (!rc)
-    groth16_assemble(pk->alpha_g1, pk->beta_g1, pk->delta_g1, pk->beta_g2, pk->delta_g2, pk->a0, pk->b1_0, pk->b2_0,
-                     h_acc, l_acc, a_acc, b1_acc, b2_acc, pj->r, pj->s, a_out, b_out, c_out);
+  if (!rc) {
+    groth16_asm_c(l_acc, h_acc, &pj->asm_st, a_out, c_out);
+    memcpy(b_out, b_tmp, sizeof(b_tmp));
+  }
   delete pj;
   return rc;
 }

@@ -1490,6 +1490,9 @@ __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
     k_acc_items_g1(const uint4* __restrict__ items, const uint32_t* __restrict__ nover, uint32_t nmain,
                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases, uint32_t tn,
                    uint32_t tskip, uint32_t* __restrict__ buckets, uint32_t* __restrict__ xpts) {
+#ifdef ZK_ACC_VPAD
+  asm volatile("" ::: "v135");  // (experiment: 136 VGPRs -> three waves per SIMD)
+#endif
   acc_items_g1f(items, nover, nmain, sval, bases, tn, tskip, buckets, xpts, blockIdx.x * blockDim.x + threadIdx.x);
 }
 // (Tried for the 3-lane pipeline: rows staged through LDS by
@@ -2900,14 +2903,21 @@ struct BrGeom {
   int sr, sc, sb, segt;
   int mc = 64;  // mode 1: lanes per column segment (k_msm_br_strip)
 };
-static BrGeom br_geom(const MsmPlan& P, bool g2) {
-  // buckets folded per lane before the tree: G1 8 (16 with two 512-bucket
-  // columns per wave measured slower: 2^20 one lane 0.38 -> 0.46 ms); G2 16
-  // (2^20 G2 MSM, 2 lanes: 4.50 -> 4.17 ms)
+static BrGeom br_geom(const MsmPlan& P, bool g2, bool pipelined) {
+  // buckets folded per lane before the tree: G2 16 (2^20 G2 MSM, 2 lanes:
+  // 4.50 -> 4.17 ms).  G1: 8 on one lane, where the reduction's latency is
+  // exposed (16 with two 512-bucket columns per wave: 2^20 one lane 1.56 ->
+  // 1.62 ms per MSM); 16 when several lanes are in flight, where the
+  // reduction runs beside another lane's accumulation and what it costs is
+  // its VALU issue -- the in-wave tree's idle lanes -- rather than its latency
+  // (22K instead of 29K wave-additions per 2^19-bucket window: 2^20 table
+  // MSM, 3 lanes 895-897 -> 906-909 Mpt/s, 2 lanes 886-890 -> 911).  A sharded
+  // MSM keeps 8 on every rank: the bit-sum segments are part of the
+  // exchanged plan.
 #ifndef ZK_BR_FOLD_G1
 #define ZK_BR_FOLD_G1 8
 #endif
-  const int fold = g2 ? 16 : ZK_BR_FOLD_G1;
+  const int fold = g2 || pipelined ? 16 : ZK_BR_FOLD_G1;
   BrGeom g;
   g.mode = P.hb >= 9 ? 1 : 0;
   g.segt = 256;
@@ -3032,11 +3042,18 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
       auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
 #ifndef ZK_ACC_LDS_KB
-#define ZK_ACC_LDS_KB 0
+#define ZK_ACC_LDS_KB 41
 #endif
-      // (ZK_ACC_LDS_KB: LDS reserved per accumulation workgroup, which caps
-      // its waves per SIMD -- 41 KB: three workgroups per CU)
-      kern<<<(unsigned)((items_max + 255) / 256), 256, (size_t)ZK_ACC_LDS_KB * 1024, st>>>(
+      // 41 KB of (unused) LDS per G1 accumulation workgroup caps it at three
+      // workgroups per CU -- three of its 127-VGPR waves per SIMD instead of
+      // four -- and leaves each SIMD a wave slot the other lanes' sorts and
+      // reductions start in at once, instead of waiting for accumulation
+      // workgroups to retire.  Measured (2^20 table MSM): one lane level
+      // (1.552-1.567 vs 1.557 ms, the accumulation is issue-bound at three
+      // waves), 3 lanes 851-861 -> 886-908 Mpt/s, 2 lanes 753-757 -> 879-899.
+      // (G2's 252-VGPR waves are two per SIMD either way.)
+      const size_t acc_lds = G::CW == 8 ? (size_t)ZK_ACC_LDS_KB * 1024 : 0;
+      kern<<<(unsigned)((items_max + 255) / 256), 256, acc_lds, st>>>(
           items, &itc[0], (uint32_t)g.nmain, sval, d_bases, tn, tskip, buckets, xpts);
     }
     ZK_HIP(hipEventRecord(lane->acc_done, st));
@@ -3113,7 +3130,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
   // 1.37 ms with one shared br stream.)
   hipStream_t brs = st;
   uint32_t *Cb, *Db, *sums;
-  const BrGeom bg = br_geom(P, G::CW != 8);
+  const BrGeom bg = br_geom(P, G::CW != 8, ctx->msm_lanes > 1 && !job->comm);
   const int sr = bg.sr, sc = bg.sc, sb = bg.sb;
   ZK_TRY(ws.get("msm_C", (size_t)W * (1u << hb) * sr * XW * 4, (void**)&Cb));
   ZK_TRY(ws.get("msm_D", (size_t)W * (1u << lb) * sc * XW * 4, (void**)&Db));
@@ -3387,7 +3404,7 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
     if (n) rc = check_size(P, n);
   }
   if (!rc && n) {
-    const BrGeom bg = br_geom(P, b->g2 != 0);
+    const BrGeom bg = br_geom(P, b->g2 != 0, false);
     if ((size_t)P.W * (P.bb + 1) * bg.sb * XW + SHARD_STATUS_WORDS > SHARD_PAYLOAD_WORDS) {
       set_error("msm_sharded: window %d's bit sums exceed the sharded exchange (use a table or a window <= 20)", P.c);
       rc = ZKMI_EINVAL;

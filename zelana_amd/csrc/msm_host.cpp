@@ -137,45 +137,101 @@ static HX<F> pt(const uint64_t* aff) {
 }
 static bool is_zero4(const uint64_t k[4]) { return (k[0] | k[1] | k[2] | k[3]) == 0; }
 
+// Joint k1 P1 + k2 P2 (Straus, 4-bit windows): one doubling chain for both.
+template <class F>
+static HX<F> smul2(const HX<F>& p1, const uint64_t k1[4], const HX<F>& p2, const uint64_t k2[4]) {
+  HX<F> t1[16], t2[16];
+  t1[0] = t2[0] = xyzz_inf<F>();
+  t1[1] = p1;
+  t2[1] = p2;
+  for (int i = 2; i < 16; i++) {
+    t1[i] = xyzz_add(t1[i - 1], p1);
+    t2[i] = xyzz_add(t2[i - 1], p2);
+  }
+  HX<F> acc = xyzz_inf<F>();
+  for (int w = 63; w >= 0; w--) {
+    for (int d = 0; d < 4; d++) acc = xyzz_dbl(acc);
+    const int d1 = (int)((k1[w / 16] >> (4 * (w % 16))) & 15), d2 = (int)((k2[w / 16] >> (4 * (w % 16))) & 15);
+    if (d1) acc = xyzz_add(acc, t1[d1]);
+    if (d2) acc = xyzz_add(acc, t2[d2]);
+  }
+  return acc;
+}
+template <class F, int K>
+static void st_hx(uint64_t* o, const HX<F>& p) {
+  memcpy(o, &p, sizeof(HX<F>));
+  static_assert(sizeof(HX<F>) == 4 * K * 8, "host XYZZ layout");
+}
+template <class F, int K>
+static HX<F> ld_hx(const uint64_t* o) {
+  HX<F> p;
+  memcpy(&p, o, sizeof(HX<F>));
+  return p;
+}
+
+// Groth16 assembly in three stages (ark-groth16 0.5 prover.rs
+// create_proof_with_reduction_and_matrices), regrouped so
+// that most of it runs while the GPU still works on the proof:
+//   A  = r delta_1 + a0 + sum z a + alpha
+//   B  = s delta_2 + b2_0 + sum z b_2 + beta_2
+//   B1 = s delta_1 + B1',  B1' = b1_0 + sum z b_1 + beta_1   (ark: only if r != 0)
+//   C  = s A + r B1 - r s delta_1 + l + h  =  s A + r B1' + l + h
+// (r B1 - r s delta_1 = r B1'; with r = 0 both sides drop the term).  The
+// group law is exact, so the affine A, B, C are the same field elements.
+// Stage 1 (fixed): r delta_1, s delta_2 -- right after the submit, while the
+// GPU runs the proof.  Stage 2 (after the a and b_g1 MSMs): A and s A + r B1'
+// in one joint chain.  Then B (after b_g2) and C (after l and h): a few
+// additions and an affine conversion each.  (configs[0]: the one-piece
+// assembly cost ~2.1 ms of host time after the last MSM on this image's
+// container CPU; staged, ~0.2 ms of it follows the last MSM.)
+void groth16_asm_fixed(const uint64_t delta_g1[8], const uint64_t delta_g2[16], const uint64_t r[4],
+                       const uint64_t s[4], G16Asm* st) {
+  st_hx<HFq, 4>(st->rd1, smul<HFq, 4>(delta_g1, r));
+  st_hx<HFq2, 8>(st->sd2, smul<HFq2, 8>(delta_g2, s));
+}
+void groth16_asm_ab(const uint64_t alpha_g1[8], const uint64_t beta_g1[8], const uint64_t a0[8],
+                    const uint64_t b1_0[8], const uint64_t a_acc[8], const uint64_t b1_acc[8], const uint64_t r[4],
+                    const uint64_t s[4], G16Asm* st) {
+  HX<HFq> A = ld_hx<HFq, 4>(st->rd1);
+  A = xyzz_add(A, pt<HFq, 4>(a0));
+  A = xyzz_add(A, pt<HFq, 4>(a_acc));
+  A = xyzz_add(A, pt<HFq, 4>(alpha_g1));
+  HX<HFq> B1p = xyzz_inf<HFq>();
+  if (!is_zero4(r)) {
+    B1p = xyzz_add(pt<HFq, 4>(b1_0), pt<HFq, 4>(b1_acc));
+    B1p = xyzz_add(B1p, pt<HFq, 4>(beta_g1));
+  }
+  to_affine<HFq, 8>(A, st->a_aff);
+  st_hx<HFq, 4>(st->c_part, smul2<HFq>(A, s, B1p, r));
+}
+void groth16_asm_b(const uint64_t beta_g2[16], const uint64_t b2_0[16], const uint64_t b2_acc[16], const G16Asm* st,
+                   uint64_t b_out[16]) {
+  HX<HFq2> B = ld_hx<HFq2, 8>(st->sd2);
+  B = xyzz_add(B, pt<HFq2, 8>(b2_0));
+  B = xyzz_add(B, pt<HFq2, 8>(b2_acc));
+  B = xyzz_add(B, pt<HFq2, 8>(beta_g2));
+  to_affine<HFq2, 16>(B, b_out);
+}
+void groth16_asm_c(const uint64_t l_acc[8], const uint64_t h_acc[8], const G16Asm* st, uint64_t a_out[8],
+                   uint64_t c_out[8]) {
+  HX<HFq> C = ld_hx<HFq, 4>(st->c_part);
+  C = xyzz_add(C, pt<HFq, 4>(l_acc));
+  C = xyzz_add(C, pt<HFq, 4>(h_acc));
+  memcpy(a_out, st->a_aff, 64);
+  to_affine<HFq, 8>(C, c_out);
+}
+
 void groth16_assemble(const uint64_t alpha_g1[8], const uint64_t beta_g1[8], const uint64_t delta_g1[8],
                       const uint64_t beta_g2[16], const uint64_t delta_g2[16], const uint64_t a0[8],
                       const uint64_t b1_0[8], const uint64_t b2_0[16], const uint64_t h_acc[8],
                       const uint64_t l_acc[8], const uint64_t a_acc[8], const uint64_t b1_acc[8],
                       const uint64_t b2_acc[16], const uint64_t r[4], const uint64_t s[4], uint64_t a_out[8],
                       uint64_t b_out[16], uint64_t c_out[8]) {
-  // A = r delta + a_query[0] + sum z a + alpha          (calculate_coeff)
-  HX<HFq> A = smul<HFq, 4>(delta_g1, r);
-  A = xyzz_add(A, pt<HFq, 4>(a0));
-  A = xyzz_add(A, pt<HFq, 4>(a_acc));
-  A = xyzz_add(A, pt<HFq, 4>(alpha_g1));
-  // B (G2) = s delta + b_g2_query[0] + sum z b + beta
-  HX<HFq2> B = smul<HFq2, 8>(delta_g2, s);
-  B = xyzz_add(B, pt<HFq2, 8>(b2_0));
-  B = xyzz_add(B, pt<HFq2, 8>(b2_acc));
-  B = xyzz_add(B, pt<HFq2, 8>(beta_g2));
-  // B (G1), only when r != 0 (as ark-groth16)
-  HX<HFq> B1 = xyzz_inf<HFq>();
-  if (!is_zero4(r)) {
-    B1 = smul<HFq, 4>(delta_g1, s);
-    B1 = xyzz_add(B1, pt<HFq, 4>(b1_0));
-    B1 = xyzz_add(B1, pt<HFq, 4>(b1_acc));
-    B1 = xyzz_add(B1, pt<HFq, 4>(beta_g1));
-  }
-  uint64_t Aaff[8], B1aff[8], sdelta[8];
-  to_affine<HFq, 8>(A, Aaff);
-  to_affine<HFq, 8>(B1, B1aff);
-  // C = s A + r B1 - r (s delta) + l + h
-  HX<HFq> C = smul<HFq, 4>(Aaff, s);
-  C = xyzz_add(C, smul<HFq, 4>(B1aff, r));
-  to_affine<HFq, 8>(smul<HFq, 4>(delta_g1, s), sdelta);
-  HX<HFq> rsd = smul<HFq, 4>(sdelta, r);
-  rsd.y = HFq::neg(rsd.y);
-  C = xyzz_add(C, rsd);
-  C = xyzz_add(C, pt<HFq, 4>(l_acc));
-  C = xyzz_add(C, pt<HFq, 4>(h_acc));
-  memcpy(a_out, Aaff, 64);
-  to_affine<HFq2, 16>(B, b_out);
-  to_affine<HFq, 8>(C, c_out);
+  G16Asm st;
+  groth16_asm_fixed(delta_g1, delta_g2, r, s, &st);
+  groth16_asm_ab(alpha_g1, beta_g1, a0, b1_0, a_acc, b1_acc, r, s, &st);
+  groth16_asm_b(beta_g2, b2_0, b2_acc, &st, b_out);
+  groth16_asm_c(l_acc, h_acc, &st, a_out, c_out);
 }
 
 // ---------------------------------------------------------- encodings

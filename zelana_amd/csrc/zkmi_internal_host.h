@@ -17,6 +17,22 @@ void g2_compress(const uint64_t p[16], uint8_t out[64]);
 void proof_solana(const uint64_t a[8], const uint64_t b[16], const uint64_t c[8], uint8_t out[256]);
 // Groth16 proof assembly from the five MSM results (ark-groth16
 // create_proof_with_assignment); all points canonical affine, r/s canonical.
+// staged Groth16 assembly (msm_host.cpp): host XYZZ points in Montgomery words
+struct G16Asm {
+  uint64_t rd1[16];     // r delta_1
+  uint64_t sd2[32];     // s delta_2
+  uint64_t a_aff[8];    // A, affine canonical
+  uint64_t c_part[16];  // s A + r B1'
+};
+void groth16_asm_fixed(const uint64_t delta_g1[8], const uint64_t delta_g2[16], const uint64_t r[4],
+                       const uint64_t s[4], G16Asm* st);
+void groth16_asm_ab(const uint64_t alpha_g1[8], const uint64_t beta_g1[8], const uint64_t a0[8],
+                    const uint64_t b1_0[8], const uint64_t a_acc[8], const uint64_t b1_acc[8], const uint64_t r[4],
+                    const uint64_t s[4], G16Asm* st);
+void groth16_asm_b(const uint64_t beta_g2[16], const uint64_t b2_0[16], const uint64_t b2_acc[16], const G16Asm* st,
+                   uint64_t b_out[16]);
+void groth16_asm_c(const uint64_t l_acc[8], const uint64_t h_acc[8], const G16Asm* st, uint64_t a_out[8],
+                   uint64_t c_out[8]);
 void groth16_assemble(const uint64_t alpha_g1[8], const uint64_t beta_g1[8], const uint64_t delta_g1[8],
                       const uint64_t beta_g2[16], const uint64_t delta_g2[16], const uint64_t a0[8],
                       const uint64_t b1_0[8], const uint64_t b2_0[16], const uint64_t h_acc[8],
