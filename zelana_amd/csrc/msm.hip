@@ -1486,13 +1486,15 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
   if (phase == 0) acc = xyzz_inf<F>();
   st_acc<G1T>(it.w == NOSLOT ? buckets + (size_t)it.z * XW : xpts + (size_t)it.w * XW, acc);
 }
+// VPAD: the register file padded to 136 VGPRs (three waves per SIMD) instead
+// of the launch's LDS reservation (msm_acc_phase) -- for the largest sorts,
+// whose scatter workgroups need more LDS than the reservation leaves.
+template <bool VPAD>
 __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK)
     k_acc_items_g1(const uint4* __restrict__ items, const uint32_t* __restrict__ nover, uint32_t nmain,
                    const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bases, uint32_t tn,
                    uint32_t tskip, uint32_t* __restrict__ buckets, uint32_t* __restrict__ xpts) {
-#ifdef ZK_ACC_VPAD
-  asm volatile("" ::: "v135");  // (experiment: 136 VGPRs -> three waves per SIMD)
-#endif
+  if constexpr (VPAD) asm volatile("" ::: "v135");
   acc_items_g1f(items, nover, nmain, sval, bases, tn, tskip, buckets, xpts, blockIdx.x * blockDim.x + threadIdx.x);
 }
 // (Tried for the 3-lane pipeline: rows staged through LDS by
@@ -2675,7 +2677,7 @@ static BsGeom bs_geom(const MsmPlan& P, size_t n) {
   return g;
 }
 constexpr int BS_ST = 4096;  // k_bs_scatter2 entries per LDS sub-tile
-static size_t bs_lds_scatter2(const BsGeom& g) { return rs_scatter_lds(g.NLO, BS_ST) + (2 * (size_t)g.NH + 2) * 4; }
+static size_t bs_lds_scatter2(const BsGeom& g) { return rs_scatter_lds(g.NLO, BS_ST, 256) + (2 * (size_t)g.NH + 2) * 4; }
 
 template <int C, bool BAL>
 static void launch_bs_p1(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, const BsGeom& g,
@@ -2685,7 +2687,7 @@ static void launch_bs_p1(hipStream_t st, const uint32_t* sc, size_t n, int Wp, u
   uint32_t* bintot = ctr;
   uint32_t* sctot = ctr + g.NH + 16;
   if (scatter)
-    k_bs_scatter1<C, 256, BAL><<<g.nf, 256, rs_scatter_lds(g.NH, 256 * W), st>>>(
+    k_bs_scatter1<C, 256, BAL><<<g.nf, 256, rs_scatter_lds(g.NH, 256 * W, 256), st>>>(
         sc, n, Wp, B, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff, okey, oval);
   else
     k_bs_count<C, BAL><<<g.nf, 256, g.NH * 4, st>>>(sc, n, Wp, B, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff,
@@ -3040,9 +3042,13 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     if (ctx->acc_last && ctx->acc_last != lane) ZK_HIP(hipStreamWaitEvent(st, ctx->acc_last->acc_done, 0));
     {
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
-      auto kern = G::CW == 8 ? k_acc_items_g1 : k_acc_items_g2;
-#ifndef ZK_ACC_LDS_KB
-#define ZK_ACC_LDS_KB 41
+#ifndef ZK_ACC_VPAD_LOG
+#define ZK_ACC_VPAD_LOG 27
+#endif
+      const bool vpad = G::CW == 8 && Mmax >= ((size_t)1 << std::min(ZK_ACC_VPAD_LOG, 63));
+      auto kern = G::CW == 8 ? (vpad ? k_acc_items_g1<true> : k_acc_items_g1<false>) : k_acc_items_g2;
+#ifndef ZK_ACC_LDS_B
+#define ZK_ACC_LDS_B 41984
 #endif
       // 41 KB of (unused) LDS per G1 accumulation workgroup caps it at three
       // workgroups per CU -- three of its 127-VGPR waves per SIMD instead of
@@ -3052,7 +3058,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       // (1.552-1.567 vs 1.557 ms, the accumulation is issue-bound at three
       // waves), 3 lanes 851-861 -> 886-908 Mpt/s, 2 lanes 753-757 -> 879-899.
       // (G2's 252-VGPR waves are two per SIMD either way.)
-      const size_t acc_lds = G::CW == 8 ? (size_t)ZK_ACC_LDS_KB * 1024 : 0;
+      const size_t acc_lds = G::CW == 8 && !vpad ? (size_t)ZK_ACC_LDS_B : 0;
       kern<<<(unsigned)((items_max + 255) / 256), 256, acc_lds, st>>>(
           items, &itc[0], (uint32_t)g.nmain, sval, d_bases, tn, tskip, buckets, xpts);
     }
