@@ -65,7 +65,9 @@ def parse():
     ap.add_argument("--no-g2", action="store_true", help="skip the 2^20 G2 MSM side measurement")
     ap.add_argument("--no-big", action="store_true", help="skip the config-5 global 2^26 MSM (sharded over all ranks)")
     ap.add_argument("--big-log-n", type=int, default=26, help="global MSM size 2^k of the config-5 measurement")
-    ap.add_argument("--big-steps", type=int, default=5)
+    # (10 pipelined MSMs: the 2-lane pipeline's fill -- the first MSM's ~15 ms
+    # sort before any accumulation -- put ~3 ms on each of 5)
+    ap.add_argument("--big-steps", type=int, default=10)
     ap.add_argument("--depth", type=int, default=0,
                     help="MSMs in flight in the headline (default: --lanes); above it, lanes queue a second MSM")
     ap.add_argument("--timers-in-timed-region", action="store_true",

@@ -518,6 +518,11 @@ static int get_twiddles(zkmi_ctx* ctx, uint32_t logn, int inv, const uint32_t** 
 
 // Group plan of a 2^logn transform: ceil(logn / 8) groups of <= 8 stages
 // (tile = 2048 elements: 8 sub-transforms of 256, or fewer larger ones).
+// (Measured, round 5: at most 6 stages per pass -- 16 adjacent columns, 512-B
+// bursts in every strided pass, four passes at 2^24 instead of three -- 2^24
+// NTT+INTT group time 4.28-4.30 -> 5.00-5.04 ms, 2^22 1.13-1.15 -> 1.21-1.23
+// ms: the fourth pass's traffic and per-pass work cost more than the longer
+// bursts save.)
 static std::vector<uint32_t> ntt_groups(uint32_t logn) {
   int ng = (logn + 7) / 8;  // <= 8 stages per group for either tile shape
   std::vector<uint32_t> ks(ng, logn / ng);
