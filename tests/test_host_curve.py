@@ -18,3 +18,16 @@ def test_madd_g1_lazy_matches_plain(tmp_path):
                    check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
     assert out.startswith("ok ")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_staged_groth16_assembly_matches_ark_formula(tmp_path):
+    """msm_host.cpp's staged assembly (C regrouped as s A + r B1' + l + h,
+    per-key delta tables) gives ark-groth16's A, B, C, including r = 0, s = 0
+    and MSM results at infinity."""
+    exe = tmp_path / "asm_check"
+    src = os.path.join(HERE, "..", "zelana_amd", "csrc", "msm_host.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-mbmi2", "-madx", "-o", str(exe),
+                    os.path.join(HERE, "host", "asm_check.cpp"), src], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+    assert out.startswith("ok ")

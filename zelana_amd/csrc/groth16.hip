@@ -38,9 +38,17 @@ struct zkmi_pk {
   uint32_t* d_bidx = nullptr;  // kept variable indices, ascending, in [1, V)
   size_t nb_c = 0;
   std::vector<uint8_t> vk_compressed;
+  std::vector<uint64_t> asm_d1, asm_d2;  // host fixed-base tables of delta_1 / delta_2 (msm_host.cpp)
 };
 
 namespace zk {
+
+// a key's delta tables for the staged assembly, once its delta_1 / delta_2 are set
+static void pk_asm_tables(zkmi_pk* pk) {
+  pk->asm_d1.resize(groth16_asm_table_words(0));
+  pk->asm_d2.resize(groth16_asm_table_words(1));
+  groth16_asm_tables(pk->delta_g1, pk->delta_g2, pk->asm_d1.data(), pk->asm_d2.data());
+}
 
 int ntt_raw(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit);
 int ntt_raw_epi(zkmi_ctx* ctx, uint32_t* d, uint32_t logn, int inv, bool dit, int epi, const uint32_t* lo,
@@ -739,6 +747,7 @@ int pk_load(zkmi_ctx* ctx, const uint8_t* bytes, size_t len, int compressed, zkm
     pk->vk_compressed = v;
   }
   ZK_TRY(timer_flush(ctx));
+  pk_asm_tables(pk);
   *out = pk;
   return 0;
 }
@@ -958,7 +967,7 @@ int groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, co
     return rc;
   }
   // the key-only part of the assembly (r delta_1, s delta_2) while the GPU works
-  groth16_asm_fixed(pk->delta_g1, pk->delta_g2, pj->r, pj->s, &pj->asm_st);
+  groth16_asm_fixed_tab(pk->asm_d1.data(), pk->asm_d2.data(), pj->r, pj->s, &pj->asm_st);
   *out = pj;
   return 0;
 }
@@ -1057,6 +1066,7 @@ int pk_synthetic(zkmi_ctx* ctx, uint64_t seed, uint32_t log_n, size_t l, size_t 
   memcpy(pk->b1_0, t1.data(), 64);
   if ((rc = bases_export(pk->b_g2_query, t2.data()))) return fail(rc);
   memcpy(pk->b2_0, t2.data(), 128);
+  pk_asm_tables(pk);
   *out = pk;
   return 0;
 }
@@ -1288,6 +1298,7 @@ int groth16_setup(zkmi_ctx* ctx, const zkmi_r1cs* cs, const uint64_t tw[20], con
   for (size_t i = 0; i < l; i++) g1_compress(&pk->gamma_abc[i * 8], v.data() + 232 + i * 32);
   pk->vk_compressed = v;
   if ((rc = timer_flush(ctx))) return fail(rc);
+  pk_asm_tables(pk);
   *out = pk;
   return 0;
 }

@@ -1,6 +1,7 @@
 // zkmi_internal_host.h — host-only helpers of libzkmi.so (no HIP dependency;
 // compiled by g++ in msm_host.cpp).
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace zk {
@@ -26,6 +27,10 @@ struct G16Asm {
 };
 void groth16_asm_fixed(const uint64_t delta_g1[8], const uint64_t delta_g2[16], const uint64_t r[4],
                        const uint64_t s[4], G16Asm* st);
+size_t groth16_asm_table_words(int g2);
+void groth16_asm_tables(const uint64_t delta_g1[8], const uint64_t delta_g2[16], uint64_t* tab1, uint64_t* tab2);
+void groth16_asm_fixed_tab(const uint64_t* tab1, const uint64_t* tab2, const uint64_t r[4], const uint64_t s[4],
+                           G16Asm* st);
 void groth16_asm_ab(const uint64_t alpha_g1[8], const uint64_t beta_g1[8], const uint64_t a0[8],
                     const uint64_t b1_0[8], const uint64_t a_acc[8], const uint64_t b1_acc[8], const uint64_t r[4],
                     const uint64_t s[4], G16Asm* st);
