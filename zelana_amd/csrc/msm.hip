@@ -52,6 +52,10 @@ namespace zk {
 // because the 1024-thread P1 scatter and the 152-VGPR reductions still wait
 // for accumulation waves to retire -- a register / LDS footprint matter,
 // DESIGN.md §2.1.)
+// (Round 5, with the tails running beside the LDS-capped accumulation: tail
+// priority 0 / 1 instead of 3 measured 864-866 / 875-880 vs 869-880 Mpt/s at
+// 2-3 lanes and 67.7 / 65.9 vs 65.7 ms at 2^26 -- the sort's slack does not
+// buy the accumulation anything.)
 #define ZK_TAIL_WAVE() __builtin_amdgcn_s_setprio(3)
 
 // ----------------------------------------------------------------- traits
