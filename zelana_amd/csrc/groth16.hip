@@ -874,7 +874,11 @@ namespace zk {
 // fork from one event recorded before the witness map, so they run beside it.
 // (A hipGraph capture of the whole small proof -- one replay launch instead
 // of ~140 -- measured 3.36 ms against 3.12 ms enqueued as streams: the
-// replayed DAG loses more lane overlap than the launches cost; dropped.)
+// replayed DAG loses more lane overlap than the launches cost; dropped.
+// Round 5: b_g2 accumulated on the other lane from a copy of the shared sort
+// -- lane 0 b_g1, l, a; lane 1 b_g2, h -- measured 1.88-1.98 ms against
+// 1.74-1.83 for this order; with three lanes the third lane's stream shared a
+// hardware queue (GPU_MAX_HW_QUEUES = 4 with the context stream), 2.05 ms.)
 constexpr size_t SMALL_PROOF_MAX = (size_t)1 << 16;  // domains up to which the small schedule applies
 static int prove_submit_small(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, const uint32_t* dz,
                               uint32_t logn, uint32_t* dh, zkmi_msm_job** jobs) {
