@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--l2-steps", type=int, default=8)
     ap.add_argument("--no-zbatch", action="store_true", help="skip the zelana_batch (batch 70) proof measurement")
     ap.add_argument("--no-g2", action="store_true", help="skip the 2^20 G2 MSM side measurement")
+    ap.add_argument("--no-window-ab", action="store_true",
+                    help="skip the plain-MSM point-shard vs window-shard A/B")
+    ap.add_argument("--window-ab-log-n", type=int, default=24)
     ap.add_argument("--no-big", action="store_true", help="skip the config-5 global 2^26 MSM (sharded over all ranks)")
     ap.add_argument("--big-log-n", type=int, default=26, help="global MSM size 2^k of the config-5 measurement")
     # (10 pipelined MSMs: the 2-lane pipeline's fill -- the first MSM's ~15 ms
@@ -262,6 +265,10 @@ def main():
             allgather, big_state)
         if comm is not None:
             extra["msm_exchange"]["per_rank"] = extra["msm_global_2_%d" % args.big_log_n].get("per_rank")
+    if not args.no_window_ab:
+        log("plain MSM 2^%d: point vs window shards" % args.window_ab_log_n)
+        extra["msm_plain_point_vs_window_2_%d" % args.window_ab_log_n] = bench_window_vs_point(
+            ctx, comm, args.window_ab_log_n, 5, world, rank, sync_all, allmax)
     if not args.no_g2:
         log("G2 MSM 2^%d" % args.log_n)
         extra["msm_g2_2_%d" % args.log_n] = bench_msm_g2(ctx, args.log_n, max(4, args.steps // 2), rank, world,
@@ -383,6 +390,52 @@ def pipelined(submit, finish, k, depth):
     while q:
         res = finish(q.popleft())
     return res
+
+
+def bench_window_vs_point(ctx, comm, log_n, steps, world, rank, sync_all, allmax):
+    """north_star's two ways to shard one plain-Pippenger MSM,
+    A/B on the same 2^log_n set, c = 16 (16 windows), no fixed-base table:
+    point shards (rank r runs all windows over elements [r N/W, (r+1) N/W))
+    against window shards (every rank holds all N points and scalars and runs
+    windows [r 16/W, (r+1) 16/W)); the same fixed-size exchange, every rank's
+    result is the whole MSM.  At N = 1 both are the same computation (a
+    one-rank host communicator); the A/B is the driver's N > 1 runs."""
+    import hashlib
+
+    from zelana_amd import gpu
+
+    total = 1 << log_n
+    b = ctx.bases_generate(seed=1024, n=total)
+    s = ctx.scalars_generate(seed=24, n=total)
+    own = None
+    if comm is None:
+        own = comm = gpu.Comm.host(ctx, 1, 0, lambda blob: [blob])
+    first, cnt = gpu.shard_range(total, world, rank)
+    sv = s.view(first * 32, cnt * 32)
+    ctx.set_window(16)
+    modes = {"point_sharded": lambda: comm.msm_submit(b, sv, cnt, offset=first),
+             "window_sharded": lambda: comm.msm_windows_submit(b, s, total)}
+    out, res = {}, {}
+    for name, sub in modes.items():
+        pipelined(sub, ctx.msm_wait, 4, 2)  # lanes warm
+        sync_all()
+        t0 = time.perf_counter()
+        res[name] = pipelined(sub, ctx.msm_wait, steps, 2)
+        dt = allmax(time.perf_counter() - t0)
+        out[name] = {"value": round(total * steps / dt / 1e6, 2), "unit": "Mpoint-scalar/s",
+                     "ms_per_msm": round(dt / steps * 1e3, 3)}
+    ctx.set_window(0)
+    if own is not None:
+        own.close()
+    r0 = np.asarray(res["point_sharded"])
+    out.update({
+        "workload": f"plain Pippenger (c = 16, no table) BN254 G1 MSM 2^{log_n}, {world} rank(s); "
+                    "point shards vs window shards of the same MSM (zkmi_msm_window_sharded_submit)",
+        "steps": steps, "n_gpus": world, "scaling": "strong",
+        "same_result": bool(np.array_equal(r0, np.asarray(res["window_sharded"]))),
+        "result_sha256": hashlib.sha256(r0.tobytes()).hexdigest()[:16],
+    })
+    return out
 
 
 def msm_inputs(ctx, kind, scalar_seed, point_seed, n, first=0, splitmix_point_seed=None):

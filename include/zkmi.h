@@ -202,6 +202,18 @@ int zkmi_msm_sharded_submit(zkmi_comm* comm, const zkmi_bases* shard, size_t off
                             size_t n, zkmi_msm_job** job);
 int zkmi_msm_sharded(zkmi_comm* comm, const zkmi_bases* shard, size_t offset, const void* d_scalars, size_t n,
                      uint64_t* out_affine);
+/* Window sharding (north_star's "Pippenger windows sharded across GPUs"):
+ * every rank passes the WHOLE base set and scalars (n points, resident on its
+ * GPU) and runs windows [r W / N, (r + 1) W / N) of the plain Pippenger plan
+ * (window c = zkmi_msm_set_window, or the automatic choice; 12..22 bits; a
+ * fixed-base table is not used -- it folds every window into one).  The same
+ * fixed-size exchange as the point-sharded MSM hands each rank's window bit
+ * sums to every rank, and zkmi_msm_wait assembles all W windows (each from
+ * the one rank that ran it) before the Horner epilogue: every rank returns
+ * the whole MSM.  Collective, like zkmi_msm_sharded_submit.  Replaces the
+ * same call site (prover.rs:408 via ark-ec msm_bigint). */
+int zkmi_msm_window_sharded_submit(zkmi_comm* comm, const zkmi_bases* bases, size_t offset, const void* d_scalars,
+                                   size_t n, zkmi_msm_job** job);
 
 /* ------------------------------------------------------------- NTT */
 /* In-place radix-2 transform over Fr of length 2^log_n, natural order in and

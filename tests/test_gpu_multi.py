@@ -8,7 +8,10 @@ section; SURVEY.md §8e, BASELINE.json configs[4]).
   all-gather / epilogue path; the N-rank exchange itself is RCCL's);
 * two ranks in one process (one host thread per rank, as a Rust host with one
   thread per GPU would run them) over the host transport from Python;
-* the context device guard: a context driven from another thread.
+* the context device guard: a context driven from another thread;
+* window sharding (every rank holds the whole MSM and runs a share of the
+  plain plan's windows), G1 and G2, uneven splits, a rank without windows,
+  and ranks whose window plans disagree.
 
 Every sharded result must equal the one-rank MSM over the whole set."""
 import os
@@ -222,3 +225,86 @@ def test_stream_budget_with_communicator():
         assert c.stream_count() == 3
     finally:
         c.close()
+
+
+def _window_ranks(nr, total, windows, g2=False, pseed=1031, sseed=31):
+    """nr rank threads, each with its own context holding the WHOLE base set
+    and scalars, run a window-sharded MSM (zkmi_msm_window_sharded_submit);
+    windows[r] is rank r's window setting.  Returns (results, errors)."""
+    from zelana_amd import gpu
+    make = _thread_allgather(nr)
+    results, errors = [None] * nr, []
+
+    def rank_main(r):
+        try:
+            c = gpu.Context(0)
+            c.set_window(windows[r])
+            comm = gpu.Comm.host(c, nr, r, make(r))
+            b = c.bases_generate(seed=pseed, n=total, g2=g2)
+            s = c.scalars_generate(seed=sseed, n=total)
+            try:
+                results[r] = comm.msm_windows(b, s, total)
+            except Exception as e:
+                results[r] = repr(e)
+            del b, s
+            comm.close()
+            c.close()
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(nr)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    return results, errors
+
+
+@pytest.mark.parametrize("nr,c", [(2, 16), (3, 13), (5, 17)])
+def test_window_sharded_msm_equals_global(ctx, nr, c):
+    """north_star's window-sharding variant: every rank holds
+    all points and scalars and runs windows [r W / N, (r + 1) W / N) of the
+    plain plan (c = 16: 16 windows over 2 ranks; c = 13: 20 over 3, uneven;
+    c = 17: 15 over 5); every rank's result equals the one-rank MSM."""
+    total = 3 * (1 << 14) + 5
+    b = ctx.bases_generate(seed=1031, n=total)
+    s = ctx.scalars_generate(seed=31, n=total)
+    want = ctx.msm(b, s)
+    del b, s
+    results, errors = _window_ranks(nr, total, [c] * nr)
+    assert not errors, errors
+    for r in range(nr):
+        assert isinstance(results[r], np.ndarray), results[r]
+        assert np.array_equal(results[r], want), r
+
+
+def test_window_sharded_g2_and_empty_rank(ctx):
+    """G2 window shards (c = 17: 15 windows over 4 ranks, uneven) -- and a
+    rank left without windows (16 ranks over 15 windows) still joins the
+    exchange and returns the whole MSM."""
+    total = (1 << 12) + 3
+    b = ctx.bases_generate(seed=1033, n=total, g2=True)
+    s = ctx.scalars_generate(seed=33, n=total)
+    want = ctx.msm(b, s)
+    del b, s
+    results, errors = _window_ranks(4, total, [17] * 4, g2=True, pseed=1033, sseed=33)
+    assert not errors, errors
+    for r in range(4):
+        assert isinstance(results[r], np.ndarray) and np.array_equal(results[r], want), (r, results[r])
+    b = ctx.bases_generate(seed=1034, n=total)
+    s = ctx.scalars_generate(seed=34, n=total)
+    want = ctx.msm(b, s)
+    del b, s
+    results, errors = _window_ranks(16, total, [17] * 16, pseed=1034, sseed=34)
+    assert not errors, errors
+    for r in range(16):
+        assert isinstance(results[r], np.ndarray) and np.array_equal(results[r], want), (r, results[r])
+
+
+def test_window_sharded_mismatched_windows_fail_everywhere(ctx):
+    """Ranks that split different window plans (c = 16 on one, 14 on the
+    other) all fail in their wait -- no hang, no wrong sum."""
+    results, errors = _window_ranks(2, 5000, [16, 14])
+    assert not errors, errors
+    for r in range(2):
+        assert isinstance(results[r], str), results[r]

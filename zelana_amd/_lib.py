@@ -86,6 +86,7 @@ SIGNATURES = [
     ("zkmi_comm_info", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int)]),
     ("zkmi_shard_range", ctypes.c_int, [sz, ctypes.c_int, ctypes.c_int, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
     ("zkmi_msm_sharded_submit", ctypes.c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp)]),
+    ("zkmi_msm_window_sharded_submit", ctypes.c_int, [vp, vp, sz, vp, sz, ctypes.POINTER(vp)]),
     ("zkmi_msm_sharded", ctypes.c_int, [vp, vp, sz, vp, sz, u64p]),
     ("zkmi_g1_add", ctypes.c_int, [u64p, u64p, u64p]),
     ("zkmi_g2_add", ctypes.c_int, [u64p, u64p, u64p]),

@@ -254,6 +254,16 @@ int zkmi_msm_sharded_submit(zkmi_comm* comm, const zkmi_bases* shard, size_t off
   return msm_submit_sharded(comm, shard, offset, d_scalars, n, job);
 }
 
+int zkmi_msm_window_sharded_submit(zkmi_comm* comm, const zkmi_bases* bases, size_t offset, const void* d_scalars,
+                                   size_t n, zkmi_msm_job** job) {
+  if (!comm || !bases || !job || (n && !d_scalars)) {
+    set_error("zkmi_msm_window_sharded_submit: bad arguments");
+    return ZKMI_EINVAL;
+  }
+  ZK_DEVICE_GUARD(comm->ctx);
+  return msm_submit_sharded(comm, bases, offset, d_scalars, n, job, true);
+}
+
 int zkmi_msm_sharded(zkmi_comm* comm, const zkmi_bases* shard, size_t offset, const void* d_scalars, size_t n,
                      uint64_t* out_affine) {
   zkmi_msm_job* job = nullptr;

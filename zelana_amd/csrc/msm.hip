@@ -408,17 +408,21 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_p1_scatter(const int32_t* __r
 // a P1 chunk is CS scalars.  No digits array: its write and two reads go
 // (2^26 table MSM: 3.2 GB written + 6.4 GB read).
 template <int C, bool BAL>
+// wsel (window-sharded MSMs, plain plans): windows [w0, w0 + wn) only, keyed
+// from window w0 on (wsel = w0 | wn << 16; 0 = every window)
 __device__ __forceinline__ void rs_scalar_keys(const uint32_t* __restrict__ scalars, size_t i, size_t n, int Wp,
-                                               uint32_t B, uint32_t* key, uint32_t* val, bool* ok) {
+                                               uint32_t B, uint32_t* key, uint32_t* val, bool* ok, uint32_t wsel) {
   constexpr int W = msm_windows(C);
   int32_t d[W];
   scalar_digits<C, BAL>(scalars, i, d);
+  const uint32_t w0 = wsel & 0xFFFFu, wn = wsel >> 16;
   uint32_t j = 0, wq = 0;
 #pragma unroll
   for (int w = 0; w < W; w++) {
     const int32_t v = d[w];
-    ok[w] = v != 0;
-    key[w] = wq * B + (uint32_t)(v < 0 ? -v : v) - 1;
+    const uint32_t wr = (uint32_t)w - w0;
+    ok[w] = v != 0 && (wn == 0 || wr < wn);
+    key[w] = (wn ? wr : wq) * B + (uint32_t)(v < 0 ? -v : v) - 1;
     val[w] = (uint32_t)(j * n + i) | (v < 0 ? 0x80000000u : 0u);
     if (++wq == (uint32_t)Wp) {
       wq = 0;
@@ -438,14 +442,14 @@ __device__ __forceinline__ void rs_scalar_keys(const uint32_t* __restrict__ scal
 constexpr size_t SMALL_SORT_MAX = (size_t)1 << 18;
 template <int C, bool BAL>
 __global__ void __launch_bounds__(256) k_ss_count(const uint32_t* __restrict__ scalars, size_t n, int Wp, uint32_t B,
-                                                  uint32_t* __restrict__ cnt) {
+                                                  uint32_t wsel, uint32_t* __restrict__ cnt) {
   ZK_TAIL_WAVE();
   constexpr int W = msm_windows(C);
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t key[W], val[W];
   bool ok[W];
-  rs_scalar_keys<C, BAL>(scalars, i, n, Wp, B, key, val, ok);
+  rs_scalar_keys<C, BAL>(scalars, i, n, Wp, B, key, val, ok, wsel);
 #pragma unroll
   for (int w = 0; w < W; w++)
     if (ok[w]) atomicAdd(&cnt[key[w]], 1u);
@@ -484,7 +488,7 @@ __global__ void __launch_bounds__(1024) k_ss_scan(const uint32_t* __restrict__ c
 }
 template <int C, bool BAL>
 __global__ void __launch_bounds__(256) k_ss_scatter(const uint32_t* __restrict__ scalars, size_t n, int Wp,
-                                                    uint32_t B, uint32_t* __restrict__ cursor,
+                                                    uint32_t B, uint32_t wsel, uint32_t* __restrict__ cursor,
                                                     uint32_t* __restrict__ sval) {
   ZK_TAIL_WAVE();
   constexpr int W = msm_windows(C);
@@ -492,7 +496,7 @@ __global__ void __launch_bounds__(256) k_ss_scatter(const uint32_t* __restrict__
   if (i >= n) return;
   uint32_t key[W], val[W];
   bool ok[W];
-  rs_scalar_keys<C, BAL>(scalars, i, n, Wp, B, key, val, ok);
+  rs_scalar_keys<C, BAL>(scalars, i, n, Wp, B, key, val, ok, wsel);
 #pragma unroll
   for (int w = 0; w < W; w++)
     if (ok[w]) sval[atomicAdd(&cursor[key[w]], 1u)] = val[w];
@@ -694,7 +698,7 @@ __device__ __forceinline__ uint32_t block_prefix(uint32_t nb, Get get, uint32_t*
 
 template <int C, bool BAL>
 __global__ void __launch_bounds__(256) k_bs_count(const uint32_t* __restrict__ scalars, size_t n, int Wp, uint32_t B,
-                                                  uint32_t NH, uint32_t lob, uint32_t CS, uint32_t scs,
+                                                  uint32_t wsel, uint32_t NH, uint32_t lob, uint32_t CS, uint32_t scs,
                                                   uint32_t* __restrict__ bintot, uint32_t* __restrict__ sctot,
                                                   uint32_t* __restrict__ choff, uint32_t* __restrict__ next_ctr,
                                                   uint32_t ctr_words) {
@@ -709,7 +713,7 @@ __global__ void __launch_bounds__(256) k_bs_count(const uint32_t* __restrict__ s
   for (uint32_t k = threadIdx.x; k < CS && base + k < n; k += 256) {
     uint32_t key[W], val[W];
     bool ok[W];
-    rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok);
+    rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok, wsel);
 #pragma unroll
     for (int w = 0; w < W; w++)
       if (ok[w]) atomicAdd(&hist[key[w] >> lob], 1u);
@@ -730,7 +734,7 @@ __global__ void __launch_bounds__(256) k_bs_count(const uint32_t* __restrict__ s
 // T threads, sub-tiles of T scalars (T * W entries)
 template <int C, int T, bool BAL>
 __global__ void __launch_bounds__(T) k_bs_scatter1(const uint32_t* __restrict__ scalars, size_t n, int Wp, uint32_t B,
-                                                   uint32_t NH, uint32_t lob, uint32_t CS, uint32_t scs,
+                                                   uint32_t wsel, uint32_t NH, uint32_t lob, uint32_t CS, uint32_t scs,
                                                    const uint32_t* __restrict__ bintot,
                                                    const uint32_t* __restrict__ sctot,
                                                    const uint32_t* __restrict__ choff, uint32_t* __restrict__ okey,
@@ -751,7 +755,7 @@ __global__ void __launch_bounds__(T) k_bs_scatter1(const uint32_t* __restrict__ 
   auto fill = [&](uint32_t sub, uint32_t* key, uint32_t* val, bool* ok) {
     const uint32_t k = sub * T + threadIdx.x;
     if (k < cnt) {
-      rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok);
+      rs_scalar_keys<C, BAL>(scalars, base + k, n, Wp, B, key, val, ok, wsel);
     } else {
 #pragma unroll
       for (int w = 0; w < W; w++) ok[w] = false;
@@ -2537,20 +2541,20 @@ static int dispatch_digits(int c, hipStream_t st, const uint32_t* sc, size_t n, 
 }
 
 template <int C, bool BAL>
-static void launch_small_sort(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t K,
+static void launch_small_sort(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t wsel, uint32_t K,
                               uint32_t* cnt, uint32_t* cursor, uint32_t* bstart, uint32_t* sval) {
   const unsigned g = (unsigned)((n + 255) / 256);
-  k_ss_count<C, BAL><<<g, 256, 0, st>>>(sc, n, Wp, B, cnt);
+  k_ss_count<C, BAL><<<g, 256, 0, st>>>(sc, n, Wp, B, wsel, cnt);
   k_ss_scan<<<1, 1024, 0, st>>>(cnt, K, bstart, cursor);
-  k_ss_scatter<C, BAL><<<g, 256, 0, st>>>(sc, n, Wp, B, cursor, sval);
+  k_ss_scatter<C, BAL><<<g, 256, 0, st>>>(sc, n, Wp, B, wsel, cursor, sval);
 }
-static int small_sort(int c, bool bal, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t K,
+static int small_sort(int c, bool bal, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t wsel, uint32_t K,
                       uint32_t* cnt, uint32_t* cursor, uint32_t* bstart, uint32_t* sval) {
   switch (c) {
 #define ZK_C(CC)                                                                     \
   case CC:                                                                           \
-    if (bal) launch_small_sort<CC, true>(st, sc, n, Wp, B, K, cnt, cursor, bstart, sval); \
-    else launch_small_sort<CC, false>(st, sc, n, Wp, B, K, cnt, cursor, bstart, sval);    \
+    if (bal) launch_small_sort<CC, true>(st, sc, n, Wp, B, wsel, K, cnt, cursor, bstart, sval); \
+    else launch_small_sort<CC, false>(st, sc, n, Wp, B, wsel, K, cnt, cursor, bstart, sval);    \
     break;
     ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15) ZK_C(16) ZK_C(17) ZK_C(18) ZK_C(19) ZK_C(20) ZK_C(21) ZK_C(22)
 #undef ZK_C
@@ -2577,6 +2581,8 @@ struct zkmi_msm_job {
   hipStream_t st = nullptr;     // lane stream the D2H of `host` is queued on
   zkmi_comm* comm = nullptr;    // sharded MSM: bit sums of every rank are summed
   bool exchanged = false;       // sharded over RCCL: the all-gather is queued
+  bool wmode = false;           // window-sharded: each rank's bit sums cover its windows only
+  int w0 = 0;                   // (window-sharded) this rank's first window
 };
 
 namespace zk {
@@ -2609,6 +2615,11 @@ struct MsmPlan {
   bool bal;  // balanced window widths (full tables built with them, WinLayout)
   size_t ne, Mmax;
   uint32_t B, K;
+  // window-sharded plain plans: this rank's windows [w0, w0 + W) of the
+  // msm_windows(c) the scalars recode into (wsel as rs_scalar_keys)
+  int w0 = 0;
+  uint32_t wsel = 0;
+  int Wp() const { return wsel ? msm_windows(c) : W; }  // windows per recoded scalar (per table copy)
 };
 static MsmPlan msm_plan(const zkmi_ctx* ctx, const zkmi_bases* tb, size_t n) {
   MsmPlan P;
@@ -2684,7 +2695,7 @@ constexpr int BS_ST = 4096;  // k_bs_scatter2 entries per LDS sub-tile
 static size_t bs_lds_scatter2(const BsGeom& g) { return rs_scatter_lds(g.NLO, BS_ST, 256) + (2 * (size_t)g.NH + 2) * 4; }
 
 template <int C, bool BAL>
-static void launch_bs_p1(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, const BsGeom& g,
+static void launch_bs_p1(hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t wsel, const BsGeom& g,
                          uint32_t* ctr, uint32_t* next_ctr, uint32_t* choff, uint32_t* okey, uint32_t* oval,
                          bool scatter) {
   constexpr int W = msm_windows(C);
@@ -2692,18 +2703,18 @@ static void launch_bs_p1(hipStream_t st, const uint32_t* sc, size_t n, int Wp, u
   uint32_t* sctot = ctr + g.NH + 16;
   if (scatter)
     k_bs_scatter1<C, 256, BAL><<<g.nf, 256, rs_scatter_lds(g.NH, 256 * W, 256), st>>>(
-        sc, n, Wp, B, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff, okey, oval);
+        sc, n, Wp, B, wsel, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff, okey, oval);
   else
-    k_bs_count<C, BAL><<<g.nf, 256, g.NH * 4, st>>>(sc, n, Wp, B, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff,
+    k_bs_count<C, BAL><<<g.nf, 256, g.NH * 4, st>>>(sc, n, Wp, B, wsel, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff,
                                                     next_ctr, (uint32_t)g.ctr_words());
 }
-static int bs_p1(int c, bool bal, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, const BsGeom& g,
+static int bs_p1(int c, bool bal, hipStream_t st, const uint32_t* sc, size_t n, int Wp, uint32_t B, uint32_t wsel, const BsGeom& g,
                  uint32_t* ctr, uint32_t* next_ctr, uint32_t* choff, uint32_t* okey, uint32_t* oval, bool scatter) {
   switch (c) {
 #define ZK_C(CC)                                                                                  \
   case CC:                                                                                        \
-    if (bal) launch_bs_p1<CC, true>(st, sc, n, Wp, B, g, ctr, next_ctr, choff, okey, oval, scatter); \
-    else launch_bs_p1<CC, false>(st, sc, n, Wp, B, g, ctr, next_ctr, choff, okey, oval, scatter);    \
+    if (bal) launch_bs_p1<CC, true>(st, sc, n, Wp, B, wsel, g, ctr, next_ctr, choff, okey, oval, scatter); \
+    else launch_bs_p1<CC, false>(st, sc, n, Wp, B, wsel, g, ctr, next_ctr, choff, okey, oval, scatter);    \
     break;
     ZK_C(12) ZK_C(13) ZK_C(14) ZK_C(15) ZK_C(16) ZK_C(17) ZK_C(18) ZK_C(19) ZK_C(20) ZK_C(21) ZK_C(22)
 #undef ZK_C
@@ -2811,8 +2822,8 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
       io.split = split;
       io.stage = stage;
     }
-    ZK_TRY(bs_p1(P.c, P.bal, st, d_scalars, n, P.W, P.B, g, ctr, next_ctr, choff, okey, oval, false));
-    ZK_TRY(bs_p1(P.c, P.bal, st, d_scalars, n, P.W, P.B, g, ctr, next_ctr, choff, okey, oval, true));
+    ZK_TRY(bs_p1(P.c, P.bal, st, d_scalars, n, P.Wp(), P.B, P.wsel, g, ctr, next_ctr, choff, okey, oval, false));
+    ZK_TRY(bs_p1(P.c, P.bal, st, d_scalars, n, P.Wp(), P.B, P.wsel, g, ctr, next_ctr, choff, okey, oval, true));
     ZK_HIP(hipEventRecord(lane->consumed, st));
     ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
     const uint32_t gt = ((g.T2max + 7) / 8) * 8;  // XCD-mapped grid (rs_xcd_tile)
@@ -2839,7 +2850,7 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
     ZK_TRY(ws.get("msm_ss_cnt", (size_t)P.K * 4, (void**)&scnt));
     ZK_TRY(ws.get("msm_ss_cursor", (size_t)P.K * 4, (void**)&scur));
     ZK_HIP(hipMemsetAsync(scnt, 0, (size_t)P.K * 4, st));
-    ZK_TRY(small_sort(P.c, P.bal, st, d_scalars, n, P.W, P.B, P.K, scnt, scur, bstart, sval));
+    ZK_TRY(small_sort(P.c, P.bal, st, d_scalars, n, P.Wp(), P.B, P.wsel, P.K, scnt, scur, bstart, sval));
     ZK_HIP(hipEventRecord(lane->consumed, st));
     ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
     ZK_HIP(hipGetLastError());
@@ -2948,8 +2959,9 @@ static BrGeom br_geom(const MsmPlan& P, bool g2, bool pipelined) {
 // non-empty shards differ.  36,864 words hold every table plan (<= 22.5K
 // words) and the plain plans of windows <= 20 (<= 34.6K words for G2).
 constexpr size_t SHARD_PAYLOAD_WORDS = 36864;
-static uint32_t shard_sig0(int g2, int c, int bb) {
-  return 0x5A000000u | ((uint32_t)g2 << 16) | ((uint32_t)c << 8) | (uint32_t)bb;
+// word 1 of a rank's status block: 0x5A | window-sharded (bit 17) | g2 (bit 16) | c | bit sums
+static uint32_t shard_sig0(int g2, int c, int bb, bool wmode = false) {
+  return 0x5A000000u | ((uint32_t)wmode << 17) | ((uint32_t)g2 << 16) | ((uint32_t)c << 8) | (uint32_t)bb;
 }
 __global__ void k_put_words(uint32_t* __restrict__ dst, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
   if (threadIdx.x < 4) dst[threadIdx.x] = threadIdx.x == 0 ? w0 : threadIdx.x == 1 ? w1 : threadIdx.x == 2 ? w2 : w3;
@@ -2976,12 +2988,14 @@ static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, hipStream_t st, zkmi
   }
   const int nr = job->comm->nranks;
   const bool empty = words == 0;
-  k_put_words<<<1, 64, 0, st>>>(d_buf, 0u, shard_sig0(job->g2, empty ? 0 : job->c, empty ? 0 : job->bb),
-                                empty ? 0u : (uint32_t)job->sb, empty ? 0u : (uint32_t)job->W);
+  k_put_words<<<1, 64, 0, st>>>(d_buf, 0u, shard_sig0(job->g2, empty ? 0 : job->c, empty ? 0 : job->bb, job->wmode),
+                                empty ? 0u : (uint32_t)job->sb,
+                                empty ? 0u : (uint32_t)job->W | ((uint32_t)job->w0 << 16));
   ZK_HIP(hipGetLastError());
   // what msm_wait reads of each rank: status + bit sums of this rank's plan
-  // (the plan every non-empty shard must share); everything for an empty shard
-  const size_t width = empty ? SHARD_PAYLOAD_WORDS : SHARD_STATUS_WORDS + words;
+  // (the plan every non-empty point shard must share); everything for an
+  // empty shard or a window-sharded MSM (whose ranks hold different counts)
+  const size_t width = empty || job->wmode ? SHARD_PAYLOAD_WORDS : SHARD_STATUS_WORDS + words;
   if (job->comm->kind == ZKMI_COMM_RCCL) {
     uint32_t* gathered;
     ZK_TRY(lane->ws.get("msm_gathered", (size_t)nr * SHARD_PAYLOAD_WORDS * 4, (void**)&gathered));
@@ -3177,7 +3191,10 @@ static int msm_acc_any(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const zkm
 }
 
 static zkmi_msm_job* new_job(zkmi_ctx* ctx, const zkmi_bases* b, const MsmPlan& P, size_t n) {
-  return new zkmi_msm_job{ctx, b->g2, P.c, P.W, P.bb, nullptr, 0, nullptr, n == 0};
+  zkmi_msm_job* j = new zkmi_msm_job{ctx, b->g2, P.c, P.W, P.bb, nullptr, 0, nullptr, n == 0};
+  j->wmode = P.wsel != 0;
+  j->w0 = P.w0;
+  return j;
 }
 
 static int check_size(const MsmPlan& P, size_t n) {
@@ -3318,7 +3335,7 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
         msm_job_free(job);
         return ZKMI_EINVAL;
       }
-      if ((stw[1] >> 16) != (0x5A00u | (uint32_t)job->g2)) {
+      if ((stw[1] >> 16) != (0x5A00u | ((uint32_t)job->wmode << 1) | (uint32_t)job->g2)) {
         set_error("msm_sharded: rank %d runs a %s MSM (or is out of step)", r, job->g2 ? "G1" : "G2");
         msm_job_free(job);
         return ZKMI_EINVAL;
@@ -3326,7 +3343,7 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
       if (((stw[1] >> 8) & 0xFF) == 0) continue;  // empty shard
       if (!ref) {
         ref = stw;
-      } else if (memcmp(ref + 1, stw + 1, 3 * sizeof(uint32_t)) != 0) {
+      } else if (memcmp(ref + 1, stw + 1, (job->wmode ? 2 : 3) * sizeof(uint32_t)) != 0) {
         set_error("msm_sharded: window plans differ between ranks (c %u/%u, windows %u/%u): use equal shards "
                   "and the same fixed-base table and window setting on every rank",
                   (ref[1] >> 8) & 0xFF, (stw[1] >> 8) & 0xFF, ref[3], stw[3]);
@@ -3343,11 +3360,28 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
     job->c = (int)((ref[1] >> 8) & 0xFF);
     job->bb = (int)(ref[1] & 0xFF);
     job->sb = (int)ref[2];
-    job->W = (int)ref[3];
-    if ((size_t)job->W * (job->bb + 1) * job->sb * XW + SHARD_STATUS_WORDS > job->host_words) {
-      set_error("msm_sharded: the agreed plan does not fit the exchanged payload");
-      msm_job_free(job);
-      return ZKMI_EINVAL;
+    job->W = job->wmode ? msm_windows(job->c) : (int)(ref[3] & 0xFFFF);
+    for (int r : live_ranks) {  // every rank's part fits the payload; window shards tile [0, W) exactly once
+      const uint32_t w3 = src[(size_t)r * job->host_words + 3];
+      if ((size_t)(w3 & 0xFFFF) * (job->bb + 1) * job->sb * XW + SHARD_STATUS_WORDS > job->host_words) {
+        set_error("msm_sharded: the agreed plan does not fit the exchanged payload");
+        msm_job_free(job);
+        return ZKMI_EINVAL;
+      }
+    }
+    if (job->wmode) {
+      std::vector<int> cover(job->W, 0);
+      for (int r : live_ranks) {
+        const uint32_t w3 = src[(size_t)r * job->host_words + 3];
+        for (uint32_t w = w3 >> 16; w < (w3 >> 16) + (w3 & 0xFFFF) && w < (uint32_t)job->W; w++) cover[w]++;
+      }
+      for (int w = 0; w < job->W; w++)
+        if (cover[w] != 1) {
+          set_error("msm_window_sharded: window %d is covered by %d ranks (every rank must split the same "
+                    "window plan)", w, cover[w]);
+          msm_job_free(job);
+          return ZKMI_EINVAL;
+        }
     }
   } else {
     live_ranks.push_back(0);
@@ -3356,16 +3390,23 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
   // terms: V_{c w + j} = U_{w,j} (j < c-1), then T_w at weight 2^{c w}
   // (each term arrives as sb segments per rank, all summed in the combine)
   int c = job->c, W = job->W, bb = job->bb, nbits = c * W, sb = job->sb;
-  const int nl = (int)live_ranks.size();
+  // point shards: every term is the sum of the ranks' terms; window shards:
+  // each window's terms come from the one rank that ran it (all-zero words
+  // elsewhere are the point at infinity)
+  const int nl = job->wmode ? 1 : (int)live_ranks.size();
   const size_t TW = (size_t)XW * sb;  // words per term and rank
   const size_t TA = TW * nl;          // words per term over the ranks summed
   std::vector<uint32_t> all((size_t)(nbits + W) * TA, 0);
-  for (int q = 0; q < nl; q++) {
-    const uint32_t* h = src + (size_t)live_ranks[q] * job->host_words + skip;
-    for (int w = 0; w < W; w++) {
+  for (int q = 0; q < (int)live_ranks.size(); q++) {
+    const uint32_t* stw = src + (size_t)live_ranks[q] * job->host_words;
+    const uint32_t* h = stw + skip;
+    const int wr0 = job->wmode ? (int)(stw[3] >> 16) : 0, wrn = job->wmode ? (int)(stw[3] & 0xFFFF) : W;
+    const size_t qo = job->wmode ? 0 : q * TW;
+    for (int w = 0; w < wrn; w++) {
+      const int wg = wr0 + w;  // global window
       for (int j = 0; j < bb; j++)
-        memcpy(&all[((size_t)c * w + j) * TA + q * TW], &h[((size_t)w * (bb + 1) + j) * TW], TW * 4);
-      memcpy(&all[((size_t)nbits + w) * TA + q * TW], &h[((size_t)w * (bb + 1) + bb) * TW], TW * 4);
+        memcpy(&all[((size_t)c * wg + j) * TA + qo], &h[((size_t)w * (bb + 1) + j) * TW], TW * 4);
+      memcpy(&all[((size_t)nbits + wg) * TA + qo], &h[((size_t)w * (bb + 1) + bb) * TW], TW * 4);
     }
   }
   if (!job->g2) msm_host_combine_g1(all.data(), nbits, W, c, sb * nl, out);
@@ -3399,7 +3440,7 @@ int msm_device(zkmi_ctx* ctx, const zkmi_bases* b, size_t offset, const void* d_
 // changed on that rank only -- entered the header exchange while its peers
 // entered the data exchange: a hang over RCCL.)
 int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
-                       zkmi_msm_job** out) {
+                       zkmi_msm_job** out, bool windows) {
   *out = nullptr;
   zkmi_ctx* ctx = comm->ctx;
   int rc = check_range(b, offset, n);
@@ -3409,7 +3450,32 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
   }
   const int XW = b->g2 ? 64 : 32;
   MsmPlan P{};
-  if (!rc) {
+  if (!rc && windows) {
+    // window sharding (north_star's variant): every rank holds every base and
+    // scalar and runs windows [r W / N, (r + 1) W / N) of the plain plan (no
+    // fixed-base table: a table folds all windows into one)
+    P.c = ctx->msm_window > 0 ? ctx->msm_window : pick_window(n);
+    if (P.c < 12 || P.c > 22) {
+      set_error("msm_window_sharded: window %d outside 12..22 (zkmi_msm_set_window)", P.c);
+      rc = ZKMI_EINVAL;
+    } else {
+      const int Wt = msm_windows(P.c), nr = comm->nranks, r = comm->rank;
+      P.w0 = (int)((long)r * Wt / nr);
+      P.W = (int)((long)(r + 1) * Wt / nr) - P.w0;
+      P.p = 1;
+      P.bal = false;
+      P.ne = n;
+      P.Mmax = (size_t)P.W * n;
+      P.B = 1u << (P.c - 1);
+      P.K = (uint32_t)P.W * P.B;
+      P.bb = P.c - 1;
+      P.lb = (P.bb + 1) / 2;
+      P.hb = P.bb - P.lb;
+      P.wsel = (uint32_t)P.w0 | ((uint32_t)P.W << 16);
+      if (P.W == 0) n = 0;  // more ranks than windows: this rank's part is empty
+      if (n) rc = check_size(P, n);
+    }
+  } else if (!rc) {
     P = msm_plan(ctx, b, n);
     if (n) rc = check_size(P, n);
   }
@@ -3422,6 +3488,7 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
   }
   zkmi_msm_job* job = new_job(ctx, b, P, n);
   job->comm = comm;
+  job->wmode = windows;  // (also on a rank left without windows: its status block says so)
   job->empty = false;  // every rank takes part in the exchange, empty shard or not
   MsmLane* lane = nullptr;
   // test hook (tests/host/test_sharded_msm.cpp): ZKMI_DEBUG_SHARD_FAIL=<rank>

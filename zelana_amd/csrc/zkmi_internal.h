@@ -139,8 +139,11 @@ namespace zk {
 int comm_allgather_device(zkmi_comm* c, hipStream_t lane_st, const void* d_send, void* d_recv, size_t bytes);
 // Synchronous all-gather of host buffers (host transport only).
 int comm_allgather_host(zkmi_comm* c, const void* send, void* recv, size_t bytes);
+// windows = false: point shards (b is this rank's shard, the results are
+// summed); true: window shards (b and the scalars are the whole MSM on every
+// rank, each rank runs its share of the plain plan's windows)
 int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, const void* d_scalars, size_t n,
-                       zkmi_msm_job** out);
+                       zkmi_msm_job** out, bool windows = false);
 // A rank whose sharded MSM fails before its exchange is queued still takes
 // part in the job's exchange (`words` u32 per rank, a status block first),
 // with its failure flag set, so the other ranks fail in their msm_wait instead

@@ -309,6 +309,18 @@ class Comm:
     def msm(self, shard: "Bases", dscalars: "DeviceBuffer", n: int, offset: int = 0):
         return self.ctx.msm_wait(self.msm_submit(shard, dscalars, n, offset))
 
+    def msm_windows_submit(self, bases: "Bases", dscalars: "DeviceBuffer", n: int, offset: int = 0):
+        """Window-sharded MSM (zkmi_msm_window_sharded_submit): every rank
+        passes the whole base set and scalars and runs its share of the plain
+        plan's windows; every rank's wait returns the whole MSM."""
+        job = vp()
+        check(lib().zkmi_msm_window_sharded_submit(self.h, bases.h, offset, dscalars.ptr if n else None, n,
+                                                   ctypes.byref(job)), "zkmi_msm_window_sharded_submit")
+        return (job, bases.g2)
+
+    def msm_windows(self, bases: "Bases", dscalars: "DeviceBuffer", n: int, offset: int = 0):
+        return self.ctx.msm_wait(self.msm_windows_submit(bases, dscalars, n, offset))
+
     def close(self):
         if self.h:
             lib().zkmi_comm_destroy(self.h)
