@@ -13,7 +13,7 @@ export TMPDIR=/tmp
 HB=$!
 trap "kill $HB" EXIT
 if [ "${PART:-A}" = A ]; then
-SHORT="--no-plain --no-l2 --no-zbatch --no-big --no-g2 --no-cpu-baseline --steps 3 --warmup 1"
+SHORT="--no-plain --no-l2 --no-zbatch --no-big --no-g2 --no-window-ab --no-cpu-baseline --steps 3 --warmup 1"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
     python3 bench.py $SHORT > $OUT/pmc_fetch.json 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
