@@ -1,4 +1,5 @@
-"""Dev tool: Groth16 prove stage breakdown at domain 2^k with 1 and 2 MSM lanes."""
+"""Dev tool: Groth16 prove stage breakdown at domain 2^k per MSM lane count.
+usage: perf_l2.py [log_n]   env: LANES (comma list, default 1,2), PROFILE (0: timing only)"""
 import os
 import sys
 import time
@@ -18,11 +19,11 @@ pk.precompute()
 dev = gpu.R1CSDevice(ctx, cs)
 dz = gpu.DeviceBuffer(ctx, z.nbytes)
 dz.upload(z)
-for lanes in (1, 2):
+for lanes in [int(x) for x in os.environ.get("LANES", "1,2").split(",")]:
     ctx.set_lanes(lanes)
     gpu.groth16_prove_resident(ctx, pk, dev, dz, 1, 2)
     ctx.sync()
-    ctx.profile(True)
+    ctx.profile(os.environ.get("PROFILE", "1") != "0")
     ctx.profile_reset()
     t0 = time.perf_counter()
     for i in range(steps):
