@@ -1554,12 +1554,18 @@ __global__ void __launch_bounds__(256) k_items_place(const uint4* __restrict__ s
 }
 
 // Piece sums of the split buckets (k_bs_scatter2's split list: key, first
-// partial slot, pieces): one wave per bucket, every lane folds its strided
-// share of the pieces, then a 6-level LDS tree -- ~log2(pieces) dependent
-// additions however heavy the bucket (a witness-like MSM's bucket of the
-// digit 1 holds a large share of the entries).  One curve-addition call site
-// in one block-uniform loop, as the bucket reduction.  A uniform MSM splits
-// nothing: the launch reads the count and exits.
+// partial slot, pieces).  A block takes 4 split buckets: the ones of <= 256
+// pieces one wave each (every lane folds its strided share, then a 6-level
+// LDS tree), then every larger one with the whole block (256 lanes fold, a
+// 6-level tree per wave, 2 levels across the waves).  A witness-like MSM's
+// bucket of the digit 1 holds a large share of the entries: zelana_batch's
+// ~9K pieces took 137 dependent additions in one wave, ~42 with the block
+// (k_split_combine summed to 1.66 ms of a 12 ms proof in the round-5 trace,
+// but beside the other lane's work: batch-70 proofs/s measured level, 80.3-
+// 82.7 -> 81.2-81.5 resident, 86.5-87.1 -> 87.2-87.3 two in flight).
+// One curve-addition call site in one block-uniform step loop (a second
+// inlined copy spills G2).  A uniform MSM splits nothing: the launch reads
+// the count and exits.
 template <class G>
 __global__ void __launch_bounds__(256) k_split_combine(const uint4* __restrict__ split,
                                                        const uint32_t* __restrict__ nsplit,
@@ -1568,43 +1574,80 @@ __global__ void __launch_bounds__(256) k_split_combine(const uint4* __restrict__
   ZK_TAIL_WAVE();
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
+  constexpr uint32_t BIG = 256;  // pieces above which the whole block sums the bucket
   __shared__ Xyzz<F> sh[4][32];
-  __shared__ uint32_t nl[4];
+  __shared__ uint4 spl[4];
   const uint32_t ns = *nsplit;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (uint32_t base = blockIdx.x * 4; base < ns; base += gridDim.x * 4) {  // block-uniform
-    const uint32_t j = base + wave;
-    const bool live = j < ns;
-    const uint4 sp = live ? split[j] : make_uint4(0, 0, 0, 0);
-    if (lane == 0) nl[wave] = sp.z;
+    if (lane == 0) spl[wave] = base + wave < ns ? split[base + wave] : make_uint4(0, 0, 0, 0);
     __syncthreads();
-    const uint32_t mx = max(max(nl[0], nl[1]), max(nl[2], nl[3]));  // most pieces in the block
-    const uint32_t nload = (mx + 63) / 64;
-    uint32_t lev = 0;  // tree levels: ceil(log2(min(mx, 64))) -- 1 for the usual 2-piece buckets
-    while ((1u << lev) < min(mx, 64u)) lev++;
+    // schedule (block-uniform): phase 0 = the small buckets, one per wave;
+    // phases 1..4 = the big buckets in wave order, the whole block each
+    uint32_t mxs = 0;
+    for (int w = 0; w < 4; w++) mxs = max(mxs, spl[w].z <= BIG ? spl[w].z : 0u);
+    const uint32_t nload0 = (mxs + 63) / 64;
+    uint32_t lev0 = 0;
+    while ((1u << lev0) < min(mxs, 64u)) lev0++;
+    const uint4 mine = spl[wave];
+    const bool small = mine.z <= BIG;
     Xyzz<F> v = xyzz_inf<F>();
-    for (uint32_t step = 0; step < nload + lev; step++) {
+    int ph = 0;          // current phase
+    uint32_t st0 = 0;    // first step of the phase
+    uint32_t nload = nload0, lev = lev0, cross = 0, stride = 64;
+    uint4 cur = mine;    // the bucket of this lane's phase
+    bool mine_in = small;  // this lane takes part in the phase
+    for (uint32_t step = 0;; step++) {
+      uint32_t k = step - st0;
+      if (k >= nload + lev + cross) {  // phase end (block-uniform): store, next phase
+        if (ph == 0) {
+          if (small && mine.z && lane == 0) st_xyzz<G>(buckets + (size_t)mine.x * XW, v);
+        } else if (threadIdx.x == 0) {
+          st_xyzz<G>(buckets + (size_t)cur.x * XW, v);
+        }
+        v = xyzz_inf<F>();
+        int w = ph;  // next big bucket: waves ph.. (phase p >= 1 is wave p - 1's bucket)
+        while (w < 4 && spl[w].z <= BIG) w++;
+        if (w >= 4) break;
+        ph = w + 1;
+        cur = spl[w];
+        mine_in = true;
+        st0 = step;
+        k = 0;
+        stride = 256;
+        nload = (cur.z + 255) / 256;
+        lev = 6;
+        cross = 2;
+      }
       Xyzz<F> q;
       bool act = false;
-      if (step < nload) {
-        const uint32_t pc = lane + 64u * step;
-        if (pc < sp.z) {
-          q = ld_xyzz<G>(xpts + (size_t)(sp.y + pc) * XW);
+      if (k < nload) {
+        const uint32_t pc = (stride == 64 ? lane : threadIdx.x) + stride * k;
+        if (mine_in && pc < cur.z) {
+          q = ld_xyzz<G>(xpts + (size_t)(cur.y + pc) * XW);
           act = !xyzz_is_inf(q);
         }
-      } else {
-        const uint32_t sz = (1u << (lev - 1)) >> (step - nload);
+      } else if (k < nload + lev) {  // in-wave tree
+        const uint32_t sz = (1u << (lev - 1)) >> (k - nload);
         if (lane >= sz && lane < 2 * sz) sh[wave][lane - sz] = v;
         __syncthreads();
         if (lane < sz) {
           q = sh[wave][lane];
           act = !xyzz_is_inf(q);
         }
+      } else {  // across the waves: 4 -> 2 -> 1 (lane 0 of each wave)
+        const uint32_t sz = 2u >> (k - nload - lev);
+        if (lane == 0 && wave >= sz && wave < 2 * sz) sh[wave - sz][0] = v;
+        __syncthreads();
+        if (lane == 0 && wave < sz) {
+          q = sh[wave][0];
+          act = !xyzz_is_inf(q);
+        }
       }
       if (act) v = xyzz_is_inf(v) ? q : br_add<G>(v, q);
-      if (step >= nload) __syncthreads();
+      if (k >= nload) __syncthreads();
     }
-    if (live && lane == 0) st_xyzz<G>(buckets + (size_t)sp.x * XW, v);
+    __syncthreads();  // spl is rewritten by the next iteration
   }
 }
 
