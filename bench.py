@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--l2-steps", type=int, default=8)
     ap.add_argument("--no-zbatch", action="store_true", help="skip the zelana_batch (batch 70) proof measurement")
     ap.add_argument("--no-g2", action="store_true", help="skip the 2^20 G2 MSM side measurement")
+    ap.add_argument("--g2-lanes", type=int, default=2)
     ap.add_argument("--no-window-ab", action="store_true",
                     help="skip the plain-MSM point-shard vs window-shard A/B")
     ap.add_argument("--window-ab-log-n", type=int, default=24)
@@ -272,7 +273,7 @@ def main():
     if not args.no_g2:
         log("G2 MSM 2^%d" % args.log_n)
         extra["msm_g2_2_%d" % args.log_n] = bench_msm_g2(ctx, args.log_n, max(4, args.steps // 2), rank, world,
-                                                         sync_all, allmax)
+                                                         sync_all, allmax, lanes=args.g2_lanes)
     ntt_state = zb_state = l2_state = None
     if args.no_big:
         big_state = None
