@@ -3434,28 +3434,8 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
   const size_t skip = job->comm ? SHARD_STATUS_WORDS : 0;  // status block before each rank's bit sums
   // terms: V_{c w + j} = U_{w,j} (j < c-1), then T_w at weight 2^{c w}
   // (each term arrives as sb segments per rank, all summed in the combine)
-  int c = job->c, W = job->W, bb = job->bb, nbits = c * W, sb = job->sb;
-  // point shards: every term is the sum of the ranks' terms; window shards:
-  // each window's terms come from the one rank that ran it (all-zero words
-  // elsewhere are the point at infinity)
-  const int nl = job->wmode ? 1 : (int)live_ranks.size();
-  const size_t TW = (size_t)XW * sb;  // words per term and rank
-  const size_t TA = TW * nl;          // words per term over the ranks summed
-  std::vector<uint32_t> all((size_t)(nbits + W) * TA, 0);
-  for (int q = 0; q < (int)live_ranks.size(); q++) {
-    const uint32_t* stw = src + (size_t)live_ranks[q] * job->host_words;
-    const uint32_t* h = stw + skip;
-    const int wr0 = job->wmode ? (int)(stw[3] >> 16) : 0, wrn = job->wmode ? (int)(stw[3] & 0xFFFF) : W;
-    const size_t qo = job->wmode ? 0 : q * TW;
-    for (int w = 0; w < wrn; w++) {
-      const int wg = wr0 + w;  // global window
-      for (int j = 0; j < bb; j++)
-        memcpy(&all[((size_t)c * wg + j) * TA + qo], &h[((size_t)w * (bb + 1) + j) * TW], TW * 4);
-      memcpy(&all[((size_t)nbits + wg) * TA + qo], &h[((size_t)w * (bb + 1) + bb) * TW], TW * 4);
-    }
-  }
-  if (!job->g2) msm_host_combine_g1(all.data(), nbits, W, c, sb * nl, out);
-  else msm_host_combine_g2(all.data(), nbits, W, c, sb * nl, out);
+  msm_host_assemble_combine(src, job->host_words, skip, live_ranks.data(), (int)live_ranks.size(), job->wmode,
+                            job->g2, job->c, job->W, job->bb, job->sb, out);
   if (ctx->timer.enabled) {
     auto& t = ctx->timer.totals["msm_host_epilogue"];
     t.first += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();

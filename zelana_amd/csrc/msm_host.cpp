@@ -9,6 +9,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <vector>
+
 #include "host_field.h"
 #include "zkmi_internal_host.h"
 
@@ -112,6 +114,37 @@ void msm_host_combine_g1(const uint32_t* terms, int nbits, int W, int c, int seg
 void msm_host_combine_g2(const uint32_t* terms, int nbits, int W, int c, int seg, uint64_t out[16]) {
   combine<HFq2, 16>(terms, nbits, W, c, seg, out);
 }
+// Every rank's bit sums -> the combine's term layout -> the Horner epilogue
+// (msm.hip msm_wait; host-only so tests/host/assemble_check.cpp runs it on the
+// CPU).  payload r (at src + live[q] * stride) = a status block of `skip`
+// words (word 3: first window << 16 | windows) then its terms, rank-major:
+// window w's bb bit sums then its total, sb segments each.  Point shards:
+// every term is the sum over the ranks (sb * nl segments).  Window shards:
+// rank q's windows land at their global index, the rest stay all-zero
+// (infinity).
+void msm_host_assemble_combine(const uint32_t* src, size_t stride, size_t skip, const int* live, int nl,
+                               bool wmode, int g2, int c, int W, int bb, int sb, uint64_t* out) {
+  const int XW = g2 ? 64 : 32, nbits = c * W;
+  const int nseg = wmode ? 1 : nl;    // ranks whose segments a term sums
+  const size_t TW = (size_t)XW * sb;  // words per term and rank
+  const size_t TA = TW * nseg;        // words per term over the ranks summed
+  std::vector<uint32_t> all((size_t)(nbits + W) * TA, 0);
+  for (int q = 0; q < nl; q++) {
+    const uint32_t* stw = src + (size_t)live[q] * stride;
+    const uint32_t* h = stw + skip;
+    const int wr0 = wmode ? (int)(stw[3] >> 16) : 0, wrn = wmode ? (int)(stw[3] & 0xFFFF) : W;
+    const size_t qo = wmode ? 0 : q * TW;
+    for (int w = 0; w < wrn && wr0 + w < W; w++) {
+      const int wg = wr0 + w;  // global window
+      for (int j = 0; j < bb; j++)
+        memcpy(&all[((size_t)c * wg + j) * TA + qo], &h[((size_t)w * (bb + 1) + j) * TW], TW * 4);
+      memcpy(&all[((size_t)nbits + wg) * TA + qo], &h[((size_t)w * (bb + 1) + bb) * TW], TW * 4);
+    }
+  }
+  if (!g2) combine<HFq, 8>(all.data(), nbits, W, c, sb * nseg, out);
+  else combine<HFq2, 16>(all.data(), nbits, W, c, sb * nseg, out);
+}
+
 void host_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {
   auto r = xyzz_add(from_aff_canon<HFq, 4>(a), from_aff_canon<HFq, 4>(b));
   to_affine<HFq, 8>(r, out);

@@ -10,6 +10,10 @@ namespace zk {
 // canonical affine (all-zero = infinity).
 void msm_host_combine_g1(const uint32_t* terms, int nbits, int W, int c, int seg, uint64_t out[8]);
 void msm_host_combine_g2(const uint32_t* terms, int nbits, int W, int c, int seg, uint64_t out[16]);
+// sharded MSMs: every rank's payload (status block + bit sums) -> the
+// combine's term layout (point shards summed, window shards placed) -> Horner
+void msm_host_assemble_combine(const uint32_t* src, size_t stride, size_t skip, const int* live, int nl,
+                               bool wmode, int g2, int c, int W, int bb, int sb, uint64_t* out);
 void host_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
 void host_g2_add_affine(const uint64_t a[16], const uint64_t b[16], uint64_t out[16]);
 // arkworks compressed encodings and the Solana 256-byte proof layout
