@@ -63,7 +63,10 @@ def parse():
     ap.add_argument("--l2-steps", type=int, default=8)
     ap.add_argument("--no-zbatch", action="store_true", help="skip the zelana_batch (batch 70) proof measurement")
     ap.add_argument("--no-g2", action="store_true", help="skip the 2^20 G2 MSM side measurement")
-    ap.add_argument("--g2-lanes", type=int, default=2)
+    # (3 lanes: 2^20 G2 table MSM 311-313 -> 343-344 Mpt/s on one box; capped
+    # at 2 beside a communicator)
+    ap.add_argument("--g2-lanes", type=int, default=3)
+    ap.add_argument("--side-lanes", type=int, default=2, help="MSM lanes of the 2^26 and proof legs")
     ap.add_argument("--no-window-ab", action="store_true",
                     help="skip the plain-MSM point-shard vs window-shard A/B")
     ap.add_argument("--window-ab-log-n", type=int, default=24)
@@ -256,8 +259,9 @@ def main():
                                  "what": "all-gather of every rank's per-window bit sums inside libzkmi "
                                          "(zkmi_msm_sharded_submit), group-law sum in its epilogue"}
     # side measurements below: 2 lanes (the 2^26 MSM and the provers measured
-    # best there: their MSMs are long enough that two overlap fully)
-    ctx.set_lanes(2)
+    # best there: their MSMs are long enough that two overlap fully; round 5,
+    # 3 lanes: 2^22 proofs 34.5-34.9 -> 33.9-34.2/s, batch 70 level)
+    ctx.set_lanes(args.side_lanes)
     if not args.no_big:
         log("config 5: global 2^%d MSM" % args.big_log_n)
         big_state = {} if (rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_cpu_big) else None
@@ -552,6 +556,7 @@ def bench_msm_g2(ctx, log_n, steps, rank, world, sync_all, allmax, lanes=2):
     sc = ctx.scalars_upload(stdrng_fr(40 + rank, n))
     prev_lanes = ctx.lanes()
     ctx.set_lanes(lanes)
+    lanes = ctx.lanes()  # (capped at 2 beside a communicator)
 
     def timed(k):
         pipelined(lambda: ctx.msm_submit(bases, sc, n), ctx.msm_wait, 2 * lanes, lanes)  # lanes warm
