@@ -2689,7 +2689,14 @@ static bool same_plan(const MsmPlan& a, const MsmPlan& b) {
 // configs[0] proof's ~8K-point MSMs, 2^12 buckets -- on this path with cap 8
 // or 16: resident prove 2.95-3.02 / 3.10-3.35 ms against 2.74-2.86 ms on the
 // chunked path, round 5; they stay chunked.)
-static bool items_plan(const MsmPlan& P) { return P.K >= ITEMS_MIN_K && P.W <= 2 && P.c >= 12 && P.c <= 22; }
+// Plain (multi-window) plans take the items path too when their buckets are
+// short (<= 64 entries on average: one lane per bucket keeps its waves in
+// step): 2^20 plain MSM (16 windows, ~32 entries per bucket) 508-516 -> 537-538
+// Mpt/s; at 2^24 (~512 per bucket) the chunked path stays faster (674-687
+// against 653-656 on the items path).
+static bool items_plan(const MsmPlan& P) {
+  return P.K >= ITEMS_MIN_K && P.c >= 12 && P.c <= 22 && (P.W <= 2 || P.Mmax <= (size_t)64 * P.K);
+}
 // Piece cap of the items: no lane may run much longer than the kernel's share
 // per resident lane (~M / (CUs x 768 lanes)), or its chain becomes the tail;
 // buckets above it (witness-like 0/1 scalars, small scalars) are split and
