@@ -276,7 +276,7 @@ def main():
             ctx, comm, args.window_ab_log_n, 5, world, rank, sync_all, allmax)
     if not args.no_g2:
         log("G2 MSM 2^%d" % args.log_n)
-        extra["msm_g2_2_%d" % args.log_n] = bench_msm_g2(ctx, args.log_n, max(4, args.steps // 2), rank, world,
+        extra["msm_g2_2_%d" % args.log_n] = bench_msm_g2(ctx, args.log_n, max(4, args.steps), rank, world,
                                                          sync_all, allmax, lanes=args.g2_lanes)
     ntt_state = zb_state = l2_state = None
     if args.no_big:
