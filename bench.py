@@ -79,7 +79,11 @@ def parse():
                     help="MSMs in flight in the headline (default: --lanes); above it, lanes queue a second MSM")
     ap.add_argument("--timers-in-timed-region", action="store_true",
                     help="keep the HIP-event stage timers on while timing the headline (default: separate pass)")
-    ap.add_argument("--lanes", type=int, default=3,
+    # (round 5, with the LDS-capped accumulation the tails start beside: bench
+    # headline 877.7-886.0 with 2 lanes against 876.5-881.7 with 3, plain leg
+    # 583-590 against 470-529 Mpt/s, one box, 3 interleaved repeats; N > 1
+    # runs are capped at 2 lanes beside the communicator anyway)
+    ap.add_argument("--lanes", type=int, default=2,
                     help="MSM lanes (streams with private scratch) = MSMs kept in flight in the timed loops")
     return ap.parse_args()
 
