@@ -1,6 +1,6 @@
 """Dev tool: the bench's headline loop alone (2^20 G1 table MSM, pipelined over
 LANES lanes, profile timers OFF) for a rocprofv3 kernel trace.
-usage: headline_loop.py [log_n] [steps]   env: LANES (3), WARM (6)"""
+usage: headline_loop.py [log_n] [steps]   env: LANES (2), WARM (6)"""
 import os
 import sys
 import time
@@ -10,7 +10,7 @@ from zelana_amd.gpu import Context  # noqa: E402
 
 log_n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 30
-lanes = int(os.environ.get("LANES", "3"))
+lanes = int(os.environ.get("LANES", "2"))
 depth = int(os.environ.get("DEPTH", "0")) or lanes  # MSMs in flight
 n = 1 << log_n
 ctx = Context(0)

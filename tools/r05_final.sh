@@ -27,7 +27,7 @@ else
 timeout -k 10 700 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
     python3 bench.py --steps 20 --warmup 5 > $OUT/bench_rocprof.json 2> $OUT/bench_rocprof.err
 python3 tools/rocprof_summary.py $OUT/trace $OUT/bench_rocprof.json > $OUT/rocprof_summary.txt
-timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $OUT/loop3 -o run -- python3 tools/headline_loop.py 20 30 > $OUT/loop3.log 2>&1
+LANES=2 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $OUT/loop3 -o run -- python3 tools/headline_loop.py 20 30 > $OUT/loop3.log 2>&1
 python3 tools/acc_gaps.py $OUT/loop3/run_kernel_trace.csv > $OUT/headline_loop3_acc_gaps.txt
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/small -o run -- python3 tools/small_prove.py 5 > $OUT/small.log 2>&1
 fi
