@@ -11,7 +11,8 @@ Multi-GPU (torchrun, one process per GPU): weak scaling by point sharding.
 Every rank owns its own 2^log_n-point shard in HBM (the global MSM has
 N * 2^log_n terms); the exchange step is libzkmi's native all-gather of every
 rank's per-window bit sums (zkmi_msm_sharded_submit: ncclAllGather over xGMI
-when the backend is nccl) and the group-law sum in its epilogue.
+by default) and the group-law sum in its epilogue; torch.distributed runs on
+gloo for process control only.
 value = total point-scalar pairs processed by all ranks / max-over-ranks time.
 Config 5 (one global 2^26 MSM) is strong-scaled over the same communicator.
 Proofs (L2 scale and zelana_batch) and the NTT run as replicas at N > 1: every
@@ -83,6 +84,8 @@ def parse():
     # headline 877.7-886.0 with 2 lanes against 876.5-881.7 with 3, plain leg
     # 583-590 against 470-529 Mpt/s, one box, 3 interleaved repeats; N > 1
     # runs are capped at 2 lanes beside the communicator anyway)
+    ap.add_argument("--scalar-sets", type=int, default=2,
+                    help="independent scalar vectors the timed MSM loops alternate over")
     ap.add_argument("--lanes", type=int, default=2,
                     help="MSM lanes (streams with private scratch) = MSMs kept in flight in the timed loops")
     return ap.parse_args()
@@ -116,39 +119,41 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
-    dist = None
-    # one process per GPU; ZKMI_DIST_BACKEND=gloo (+ more ranks than GPUs) only
-    # to rehearse the multi-rank path on a 1-GPU box
-    backend = os.environ.get("ZKMI_DIST_BACKEND", "nccl")
-    ndev = max(1, torch.cuda.device_count())
-    gpu_index = local_rank % ndev
-    if world > 1:
-        import torch.distributed as dist  # noqa: F811
+    from zelana_amd.dist import CommInitError, init_world, make_comm, transport_from_env
 
-        torch.cuda.set_device(gpu_index)
-        dist.init_process_group(backend)
+    # One process per GPU.  torch.distributed is process control only (gloo,
+    # CPU tensors: rendezvous, barriers, the max-over-ranks reductions); the
+    # MSM exchange is libzkmi's own communicator -- RCCL over xGMI, or with
+    # ZKMI_DIST_BACKEND=gloo (+ more ranks than GPUs) the host transport, to
+    # rehearse the multi-rank path on a 1-GPU box.  So a rank holds exactly one
+    # RCCL communicator and the 4 streams of zkmi.h's budget.
+    transport = transport_from_env()
+    ndev = max(1, torch.cuda.device_count())  # (counts devices without initialising HIP)
+    gpu_index = local_rank % ndev
+    dist = init_world()
     from zelana_amd.gpu import Context
 
     ctx = Context(gpu_index)
     comm = None
     if dist is not None:
-        from zelana_amd.dist import CommInitError, make_comm
-
         try:
-            comm = make_comm(ctx, backend)  # libzkmi's own communicator: RCCL, or host (gloo rehearsal)
+            comm = make_comm(ctx, transport)
         except CommInitError as e:  # raised on every rank together: exit non-zero, never hang
             print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
             dist.destroy_process_group()
             sys.exit(1)
     n = 1 << args.log_n
     bases, scalars = msm_inputs(ctx, args.inputs, 20 + rank, 1020 + rank, n, splitmix_point_seed=1000 + rank)
-    dev = torch.device("cuda", gpu_index) if torch.cuda.is_available() else None
-    _coll_dev = dev if backend == "nccl" else None  # gloo collectives on host tensors
+    # A prover never sees the same scalars twice: the timed loops alternate
+    # over --scalar-sets independent scalar vectors (set 0 as above, set k the
+    # stream of seed 20 + 1000 k + rank), so no 32 MB vector stays in the MALL
+    # from one step to the next.
+    scalar_sets = [scalars] + [extra_scalars(ctx, args.inputs, 20 + 1000 * k + rank, n)
+                               for k in range(1, max(1, args.scalar_sets))]
+    _coll_dev = None  # every torch.distributed collective runs on host tensors (gloo)
 
     def sync_all():
         ctx.sync()
-        if dev is not None:
-            torch.cuda.synchronize(dev)
         if dist is not None:
             dist.barrier()
 
@@ -177,8 +182,14 @@ def main():
     lanes = ctx.lanes()  # capped at 2 beside a communicator (stream budget)
 
     def run(k):
-        """k MSM steps, pipelined: one MSM in flight per lane."""
-        return pipelined(lambda: submit(bases, scalars, n), finish, k, args.depth or lanes)
+        """k MSM steps, pipelined: one MSM in flight per lane; step i over
+        scalar set i mod len(scalar_sets).  Returns the last step's result."""
+        it = iter(range(k))
+        return pipelined(lambda: submit(bases, scalar_sets[next(it) % len(scalar_sets)], n), finish, k,
+                         args.depth or lanes)
+
+    def last_set(k):
+        return (k - 1) % len(scalar_sets)
 
     def timed(k, warm, prof=False):
         """prof: HIP-event stage timers on (the stage breakdown comes from a
@@ -227,11 +238,17 @@ def main():
     # steps: with --no-plain the first timed steps otherwise still paid for it
     run(2 * lanes)
     sync_all()
-    result, elapsed = timed(args.steps, args.warmup, prof=args.timers_in_timed_region)
+    last, elapsed = timed(args.steps, args.warmup, prof=args.timers_in_timed_region)
     if not args.timers_in_timed_region:
         _, prof_elapsed = timed(args.steps, 0, prof=True)
+    # each set's table-MSM result, untimed, through the same (at N > 1
+    # sharded, collective) submit: set 0's is what the CPU leg checks
+    set_results = [finish(submit(bases, sc, n)) for sc in scalar_sets]
+    result = set_results[0]
+    if not np.array_equal(last, set_results[last_set(args.steps)]):
+        sys.exit("bench.py: the timed loop's last MSM differs from the same MSM run alone")
     if plain is not None:
-        plain["same_result"] = bool(np.array_equal(pres, result))
+        plain["same_result"] = bool(np.array_equal(pres, set_results[last_set(max(1, args.steps // 2))]))
 
     kernel = "msm_acc0_g1"
     breakdown = stages(args.steps)
@@ -259,7 +276,9 @@ def main():
     extra = {"msm_stage_ms_per_step": breakdown, "fixed_base_table": table, "msm_plain_no_table": plain,
              "lanes": lanes}
     if comm is not None:
-        extra["msm_exchange"] = {"transport": ("rccl" if comm.info()[2] == 0 else "host:" + backend),
+        extra["msm_exchange"] = {"transport": ("rccl" if comm.info()[2] == 0 else "host:gloo"),
+                                 "process_group": dist.get_backend(),
+                                 "streams_per_rank": ctx.stream_count(),
                                  "what": "all-gather of every rank's per-window bit sums inside libzkmi "
                                          "(zkmi_msm_sharded_submit), group-law sum in its epilogue"}
     # side measurements below: 2 lanes (the 2^26 MSM and the provers measured
@@ -337,6 +356,8 @@ def main():
         "dtype": "u32",
         "data": ("synthetic, SURVEY.md §8d streams: scalars = Fr::rand of StdRng::seed_from_u64(20 + rank), points "
                  "P_i = P0 + i*D with P0, D = G1::rand of StdRng::seed_from_u64(1020 + rank); resident in HBM"
+                 + (f"; the timed steps alternate over {len(scalar_sets)} scalar vectors (set k: StdRng(20 + 1000 k "
+                    "+ rank))" if len(scalar_sets) > 1 else "")
                  if args.inputs == "stdrng" else
                  "synthetic (bases k_i*G and uniform Fr scalars from splitmix streams, generated in HBM)"),
         "config": {
@@ -445,6 +466,15 @@ def bench_window_vs_point(ctx, comm, log_n, steps, world, rank, sync_all, allmax
         "result_sha256": hashlib.sha256(r0.tobytes()).hexdigest()[:16],
     })
     return out
+
+
+def extra_scalars(ctx, kind, seed, n):
+    """Another scalar vector of the headline's kind (StdRng(seed) Fr::rand
+    draws, or the splitmix device stream of that seed)."""
+    if kind == "stdrng":
+        from zelana_amd.host_prover import stdrng_fr
+        return ctx.scalars_upload(stdrng_fr(seed, n))
+    return ctx.scalars_generate(seed=seed, n=n)
 
 
 def msm_inputs(ctx, kind, scalar_seed, point_seed, n, first=0, splitmix_point_seed=None):
@@ -662,6 +692,31 @@ def bench_ntt(ctx, log_n, world, sync_all, allmax, steps=10):
     return line, {"log_n": log_n, "x": x0, "fwd": fwd}
 
 
+def pk_load_leg(ctx, pk, prove, want):
+    """ProvingKey::deserialize_compressed at the drop-in path's size
+    (Groth16Prover::from_bytes, prover.rs:263-277; the zelana_batch key is
+    ~0.3-0.9 GB, docs/PROVER_LAYER.md:124-126): the key's compressed arkworks
+    bytes go back through zkmi_pk_load (host parse, H2D, GPU decompression
+    with the on-curve and G2 subgroup checks), and a proof under the loaded key
+    (prove(pk2), plain bases) must equal `want`, the proof under the key the
+    bytes came from."""
+    from zelana_amd import gpu
+
+    blob = pk.serialize()
+    ctx.sync()
+    t0 = time.perf_counter()
+    pk2 = gpu.ProvingKey(ctx, blob, True)
+    ctx.sync()
+    load_s = time.perf_counter() - t0
+    got = prove(pk2)
+    equal = all(np.array_equal(x, y) for x, y in zip(got, want))
+    pk2.close()
+    return {"bytes": len(blob), "load_s": round(load_s, 3), "MB_per_s": round(len(blob) / load_s / 1e6, 1),
+            "proof_equal": bool(equal),
+            "what": "zkmi_pk_load of the key's compressed arkworks bytes (validated decompression on the GPU), "
+                    "timed from host bytes to a resident key; proof under the loaded key == proof under the original"}
+
+
 def bench_l2(ctx, log_n, steps, rank, world, sync_all, allmax, keep=None):
     """Groth16 proofs/s at the config-4 scale (BASELINE.json configs[3]:
     ~2^22-constraint L2 block proof) under a REAL key: the satisfiable
@@ -754,6 +809,7 @@ def bench_l2(ctx, log_n, steps, rank, world, sync_all, allmax, keep=None):
     verifies = gpu.groth16_verify(vk, pub, *outs[0])
     pub[0] = (pub[0] + 1) % R_FR
     rejects_changed_input = not gpu.groth16_verify(vk, pub, *outs[0])
+    pk_load = pk_load_leg(ctx, pk, lambda k: gpu.groth16_prove_resident(ctx, k, dev, dz, 12345, 67890), outs[0])
     if keep is not None and world == 1:  # the CPU leg proves the same z, r, s under the oracle's setup
         z = np.zeros((prog.num_vars, 4), np.uint64)
         dz.download(z)
@@ -770,6 +826,7 @@ def bench_l2(ctx, log_n, steps, rank, world, sync_all, allmax, keep=None):
         "rejects_changed_public_input": bool(rejects_changed_input),
         "proof_equal_oracle": None,  # filled by cpu_baseline's l2_2_22 leg (rank 0, N = 1)
         "keygen_s": round(keygen_s, 2),
+        "pk_load": pk_load,
         "witness_program_ms": round(witness_ms, 2),
         "proofs_per_s": round(world / dt, 3),
         "proofs_per_s_per_gpu": round(1.0 / dt, 3),
@@ -952,6 +1009,7 @@ def bench_zbatch(ctx, steps, world, sync_all, allmax):
     ctx.sync()
     dt2 = allmax((time.perf_counter() - t0) / steps)
     two_same = all(np.array_equal(x, y) for x, y in zip(p2, proof))
+    pk_load = pk_load_leg(ctx, pk, lambda k: gpu.groth16_prove_resident(ctx, k, dev, dz, r, s), proof)
     # end to end per batch, host witness: witness (host builder), H2D of z, prove
     sync_all()
     t0 = time.perf_counter()
@@ -1062,6 +1120,7 @@ def bench_zbatch(ctx, steps, world, sync_all, allmax):
         "r1cs_and_witness_synthesis_s_host": round(synth_s, 2),
         "witness_native_mimc": zbatch._native_mimc() is not None,
         "keygen_s_gpu": round(keygen_s, 3),
+        "pk_load": pk_load,
         "table_and_upload_s": round(setup_s, 2),
         "note": "real proving key (GPU circuit_specific_setup, StdRng(0) as keygen.rs); proofs_per_s with the "
                 "witness resident in HBM",

@@ -197,7 +197,12 @@ int zkmi_comm_info(const zkmi_comm* comm, int out[3]);
  * one extra point */
 int zkmi_shard_range(size_t total, int nranks, int rank, size_t* first, size_t* count);
 /* sum over ALL ranks of sum_{i<n} scalars[i] * shard[offset + i]; collective.
- * Scalars are this rank's slice (device memory, n x 32 B canonical). */
+ * Scalars are this rank's slice (device memory, n x 32 B canonical).  A
+ * rank-local failure fails the MSM on every rank.  Over RCCL it is returned by
+ * the submit; over a host transport the submit returns a job and
+ * zkmi_msm_wait returns the error, because that transport's exchanges run in
+ * wait order (the failure joins the exchange of its own job, never an earlier
+ * job's still in flight). */
 int zkmi_msm_sharded_submit(zkmi_comm* comm, const zkmi_bases* shard, size_t offset, const void* d_scalars,
                             size_t n, zkmi_msm_job** job);
 int zkmi_msm_sharded(zkmi_comm* comm, const zkmi_bases* shard, size_t offset, const void* d_scalars, size_t n,
@@ -205,8 +210,9 @@ int zkmi_msm_sharded(zkmi_comm* comm, const zkmi_bases* shard, size_t offset, co
 /* Window sharding (north_star's "Pippenger windows sharded across GPUs"):
  * every rank passes the WHOLE base set and scalars (n points, resident on its
  * GPU) and runs windows [r W / N, (r + 1) W / N) of the plain Pippenger plan
- * (window c = zkmi_msm_set_window, or the automatic choice; 12..22 bits; a
- * fixed-base table is not used -- it folds every window into one).  The same
+ * (window c = zkmi_msm_set_window, 12..17 bits, or 0 for the automatic
+ * choice, clamped to 12..17; a fixed-base table is not used -- it folds
+ * every window into one).  The same
  * fixed-size exchange as the point-sharded MSM hands each rank's window bit
  * sums to every rank, and zkmi_msm_wait assembles all W windows (each from
  * the one rank that ran it) before the Horner epilogue: every rank returns

@@ -188,6 +188,26 @@ int run_rank(int rank, int dev, Link link, bool use_rccl) {
       if (!use_rccl)  // three exchanges, nothing else
         CHECK(link_calls - calls0 == 3, "window %d: %d host all-gathers for 3 MSMs", win, link_calls - calls0);
     }
+    // a rank-local failure between two good MSMs in flight: the
+    // failure joins its own job's exchange -- over the host transport in
+    // zkmi_msm_wait, in wait order -- so the jobs around it stay correct on
+    // both ranks and the failed one fails on both
+    {
+      zkmi_msm_job *j0 = nullptr, *j1 = nullptr, *j2 = nullptr;
+      CHECK(zkmi_msm_sharded_submit(comm, b, 0, d, count, &j0) == 0, "submit before the failure");
+      setenv("ZKMI_DEBUG_SHARD_FAIL", "0", 1);
+      int rc1 = zkmi_msm_sharded_submit(comm, b, 0, d, count, &j1);
+      unsetenv("ZKMI_DEBUG_SHARD_FAIL");
+      CHECK(zkmi_msm_sharded_submit(comm, b, 0, d, count, &j2) == 0, "submit after the failure");
+      uint64_t got[8] = {0};
+      CHECK(j0 && zkmi_msm_wait(j0, got) == 0 && memcmp(got, want, sizeof(got)) == 0,
+            "rank %d: the MSM before the in-flight failure != global", rank);
+      if (rc1 == 0) rc1 = zkmi_msm_wait(j1, got);
+      CHECK(rc1 != 0, "in-flight failure injected on rank 0: rank %d returned %d", rank, rc1);
+      memset(got, 0, sizeof(got));
+      CHECK(j2 && zkmi_msm_wait(j2, got) == 0 && memcmp(got, want, sizeof(got)) == 0,
+            "rank %d: the MSM after the in-flight failure != global", rank);
+    }
     // the window changes on rank 1 only, after MSMs of one plan ran: both
     // ranks fail (no rank waits in a collective the other skipped), and the
     // communicator stays in step

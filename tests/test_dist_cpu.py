@@ -94,3 +94,57 @@ def test_two_rank_combine():
     sc = np.concatenate([O.gen_scalars(600 + r, 300) for r in range(2)])
     want = O.msm_g1(pts, sc).tolist()
     assert res[0] == want and res[1] == want
+
+
+def _init_world_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    from zelana_amd.dist import init_world
+    dist = init_world()  # bench.py's N > 1 setup
+    import torch
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py's allmax: a host tensor over gloo
+    q.put((rank, dist.get_backend(), float(t.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_init_world_is_gloo_process_control():
+    """bench.py at N > 1 (zelana_amd.dist.init_world): torch.distributed is a
+    gloo group on host tensors -- rendezvous, barriers, the max-over-ranks
+    reduction -- never an NCCL group beside libzkmi's RCCL communicator
+    (DESIGN.md §3 stream budget)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_init_world_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(0, "gloo", 2.0), (1, "gloo", 2.0)]
+
+
+def test_make_comm_refuses_nccl_group(monkeypatch):
+    """make_comm refuses a torch NCCL process group: a second RCCL
+    communicator (and torch's NCCL stream) beside libzkmi's would break the
+    per-rank stream budget.  Checked before any GPU work, so it runs here."""
+    import torch.distributed as dist
+    from zelana_amd import dist as zd
+    monkeypatch.setenv("ZKMI_DIST_BACKEND", "gloo")
+    assert zd.transport_from_env() == "host"
+    monkeypatch.setenv("ZKMI_DIST_BACKEND", "nccl")
+    assert zd.transport_from_env() == "rccl"
+    monkeypatch.delenv("ZKMI_DIST_BACKEND")
+    assert zd.transport_from_env() == "rccl"
+    monkeypatch.setenv("ZKMI_DIST_BACKEND", "mpi")
+    with pytest.raises(ValueError):
+        zd.transport_from_env()
+    monkeypatch.setattr(dist, "get_backend", lambda group=None: "nccl")
+    for t in ("rccl", "host"):
+        with pytest.raises(zd.CommInitError, match="gloo"):
+            zd.make_comm(None, t)

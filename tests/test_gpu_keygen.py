@@ -144,6 +144,13 @@ def test_zbatch_full_keygen_prove_verify(ctx):
     same_key = gbytes == obytes.tobytes()  # (no assertion rewrite diff of 290 MB)
     assert same_key, "GPU keygen != oracle keygen at full size"
     step("GPU key bytes == oracle key bytes")
+    # Groth16Prover::from_bytes at the drop-in path's size (prover.rs:263-277,
+    # docs/PROVER_LAYER.md:124-126): the ~290 MB compressed key goes back
+    # through zkmi_pk_load (host parse, GPU decompression + on-curve / G2
+    # subgroup checks); the loaded key proves below like the generated one
+    pk_loaded = gpu.ProvingKey(ctx, gbytes, True)
+    assert (pk_loaded.n, pk_loaded.num_instance, pk_loaded.num_witness) == (pk.n, pk.num_instance, pk.num_witness)
+    step(f"loaded the {len(gbytes) / 1e6:.0f} MB compressed key")
     pk.precompute()
     step("tables built")
     rng = StdRng.seed_from_u64(int(d["batch_id"]))
@@ -156,6 +163,11 @@ def test_zbatch_full_keygen_prove_verify(ctx):
                                         O.P(oa), O.P(ob), O.P(oc), None) == 0
     O.lib().oracle_pk_free(opk)
     assert np.array_equal(a, oa) and np.array_equal(b, ob) and np.array_equal(c, oc), "GPU proof != oracle proof"
+    la, lb, lc = gpu.groth16_prove(ctx, pk_loaded, cs, z, r, s)
+    pk_loaded.close()
+    assert np.array_equal(la, oa) and np.array_equal(lb, ob) and np.array_equal(lc, oc), \
+        "proof under the loaded 290 MB key != oracle proof"
+    step("proof under the loaded key == oracle proof")
     assert gpu.proof_to_solana_bytes(a, b, c) == gpu.proof_to_solana_bytes(oa, ob, oc)
     # the product's own verifier (host pairing, zkmi_groth16_verify) accepts it
     pub_native = [O.limbs_to_int(z[i]) for i in range(1, cs.num_instance)]
@@ -236,3 +248,8 @@ def test_l2_2pow22_real_key_proof_matches_oracle(ctx):
     O.lib().oracle_pk_free(opk)
     step("oracle prove")
     assert np.array_equal(a, oa) and np.array_equal(b, ob) and np.array_equal(c, oc), "GPU proof != oracle proof"
+    la, lb, lc = gpu.groth16_prove(ctx, pk_loaded, cs, z, r, s)
+    pk_loaded.close()
+    assert np.array_equal(la, oa) and np.array_equal(lb, ob) and np.array_equal(lc, oc), \
+        "proof under the loaded 290 MB key != oracle proof"
+    step("proof under the loaded key == oracle proof")

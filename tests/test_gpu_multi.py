@@ -185,44 +185,84 @@ def test_stream_budget_with_communicator():
     holds at most GPU_MAX_HW_QUEUES = 4 streams -- the context stream, <= 2
     MSM lanes and the communicator's -- so the RCCL kernel (which waits for
     its peers) never shares a hardware queue with MSM work: lanes made before
-    the communicator beyond two are released, set_lanes is capped, and witness
-    programs run on the context stream.  Results are unchanged."""
+    the communicator beyond two are released, a witness program's own stream
+    (made by a run before the communicator) is released, set_lanes is capped,
+    and witness programs run on the context stream.  The communicator is made
+    the way bench.py makes it at N > 1 (zelana_amd.dist.init_world's gloo
+    process group + make_comm's RCCL transport, here with one rank): torch
+    holds no NCCL group of its own.  Results are unchanged."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch.distributed as dist
     from test_l2_wprog import SHAPES, _batch
     from zelana_amd import gpu, host_prover as H, wprog as W
+    from zelana_amd.dist import make_comm
     c = gpu.Context(0)
     try:
         n = 1 << 15
         b = c.bases_generate(seed=5, n=n)
         s = c.scalars_generate(seed=6, n=n)
-        c.set_lanes(3)
-        assert c.lanes() == 3
-        jobs = [c.msm_submit(b, s, n) for _ in range(3)]  # one per lane: three lane streams
-        want = [c.msm_wait(j) for j in jobs][0]
-        assert c.stream_count() == 4  # context + 3 lanes
-        comm = gpu.Comm.rccl(c, gpu.comm_unique_id(), 1, 0)
-        assert c.lanes() == 2 and c.stream_count() == 4  # context + 2 lanes + communicator
-        c.set_lanes(3)
-        assert c.lanes() == 2
-        jobs = [comm.msm_submit(b, s, n) for _ in range(4)]
-        for j in jobs:
-            assert np.array_equal(c.msm_wait(j), want)
         bal, tr, wd = SHAPES[0]
         inp, w = _batch(5, bal, tr, wd)
         _, _, plan = H.l2_record(inp, w)
         _, zh = H.native_l2_block_circuit(inp, w)
         wp = W.WitnessProgram(c, plan)
-        dz = gpu.DeviceBuffer(c, plan.num_vars * 32)
-        wp.run(H.l2_witness_inputs(inp, w), dz)
-        zg = np.zeros_like(zh)
-        dz.download(zg)
-        assert np.array_equal(zg, zh)
-        assert c.stream_count() == 4, c.stream_count()  # the program ran on the context stream
+
+        def run_program():
+            dz = gpu.DeviceBuffer(c, plan.num_vars * 32)  # fresh: a run must write all of z
+            wp.run(H.l2_witness_inputs(inp, w), dz)
+            zg = np.zeros_like(zh)
+            dz.download(zg)
+            assert np.array_equal(zg, zh)
+            dz.free()
+
+        run_program()  # before any communicator: on the program's own stream
+        assert c.stream_count() == 2, c.stream_count()  # context + program
+        c.set_lanes(3)
+        assert c.lanes() == 3
+        jobs = [c.msm_submit(b, s, n) for _ in range(3)]  # one per lane: three lane streams
+        want = [c.msm_wait(j) for j in jobs][0]
+        assert c.stream_count() == 5  # context + program + 3 lanes
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(31500 + os.getpid() % 1000))
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        try:
+            comm = make_comm(c, "rccl")  # bench.py's N > 1 path
+            assert dist.get_backend() == "gloo" and comm.info()[2] == 0
+            assert c.lanes() == 2 and c.stream_count() == 4, c.stream_count()  # context + 2 lanes + communicator
+            c.set_lanes(3)
+            assert c.lanes() == 2
+            jobs = [comm.msm_submit(b, s, n) for _ in range(4)]
+            for j in jobs:
+                assert np.array_equal(c.msm_wait(j), want)
+            run_program()
+            assert c.stream_count() == 4, c.stream_count()  # the program ran on the context stream
+            comm.close()
+            assert c.stream_count() == 3
+        finally:
+            dist.destroy_process_group()
         wp.close()
-        dz.free()
+    finally:
+        c.close()
+
+
+def test_window_sharded_rccl_one_rank():
+    """The RCCL transport of the window-sharded MSM (full-payload strided D2H,
+    the window-plan signature check) with a one-rank communicator, G1 and G2,
+    automatic and pinned windows: equals the unsharded MSM."""
+    from zelana_amd import gpu
+    c = gpu.Context(0)
+    try:
+        comm = gpu.Comm.rccl(c, gpu.comm_unique_id(), 1, 0)
+        for g2, n, win in ((False, 5000, 0), (False, 1 << 14, 13), (True, 3000, 0), (True, 4096, 12)):
+            b = c.bases_generate(seed=41 + n, n=n, g2=g2)
+            s = c.scalars_generate(seed=42 + n, n=n)
+            want = c.msm(b, s)
+            c.set_window(win)
+            got = comm.msm_windows(b, s, n)
+            c.set_window(0)
+            assert np.array_equal(got, want), (g2, n, win)
         comm.close()
-        assert c.stream_count() == 3
     finally:
         c.close()
 

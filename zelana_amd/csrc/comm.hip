@@ -137,6 +137,7 @@ static int comm_new(zkmi_ctx* ctx, int nranks, int rank, int kind, zkmi_comm** o
     }
     ctx->lane_next = 0;
   }
+  wprog_release_streams(ctx);  // witness programs run on the context stream from here on
   *out = c;
   return 0;
 }

@@ -2626,6 +2626,11 @@ struct zkmi_msm_job {
   bool exchanged = false;       // sharded over RCCL: the all-gather is queued
   bool wmode = false;           // window-sharded: each rank's bit sums cover its windows only
   int w0 = 0;                   // (window-sharded) this rank's first window
+  bool done_rec = false;        // `done` is recorded after the D2H (msm_job_free waits on it, not on st)
+  // sharded over a host transport, failed at submit: msm_wait runs the
+  // failure exchange (in wait order, as the peers' exchanges) and returns this
+  int fail_rc = 0;
+  std::string fail_msg;
 };
 
 namespace zk {
@@ -3036,6 +3041,7 @@ static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, hipStream_t st, zkmi
     job->st = st;  // from here on the pinned buffer may have a copy in flight
     ZK_HIP(hipMemcpyAsync(job->host, d_buf + SHARD_STATUS_WORDS, words * 4, hipMemcpyDeviceToHost, st));
     ZK_HIP(hipEventRecord(job->done, st));
+    job->done_rec = true;
     return 0;
   }
   const int nr = job->comm->nranks;
@@ -3065,6 +3071,7 @@ static int msm_queue_handover(zkmi_ctx* ctx, MsmLane* lane, hipStream_t st, zkmi
     ZK_HIP(hipMemcpyAsync(job->host, d_buf, width * 4, hipMemcpyDeviceToHost, st));
   }
   ZK_HIP(hipEventRecord(job->done, st));
+  job->done_rec = true;
   return 0;
 }
 
@@ -3320,8 +3327,10 @@ int msm_submit_shared(zkmi_ctx* ctx, const zkmi_bases* const* bs, int k, size_t 
 // overwritten by the stale copy.
 void msm_job_free(zkmi_msm_job* job) {
   if (!job) return;
+  // (the event, not the stream: a lane released by zkmi_comm_init after its
+  // work -- comm.hip stream budget -- may be gone while its jobs are unwaited)
   if (job->host && job->st) {
-    if (hipStreamSynchronize(job->st) != hipSuccess) {
+    if ((job->done_rec ? hipEventSynchronize(job->done) : hipStreamSynchronize(job->st)) != hipSuccess) {
       (void)hipGetLastError();
       job->host = nullptr;  // state unknown: drop the buffer rather than recycle it
     }
@@ -3339,6 +3348,13 @@ int msm_wait(zkmi_msm_job* job, uint64_t* out) {
   zkmi_ctx* ctx = job->ctx;
   ZK_DEVICE_GUARD(ctx);
   int PW = job->g2 ? 32 : 16, XW = 2 * PW;
+  if (job->fail_rc) {  // host transport: this rank's failure joins the exchange here, in wait order
+    const int frc = job->fail_rc;
+    (void)comm_fail_exchange(job->comm, SHARD_PAYLOAD_WORDS);
+    set_error("%s", job->fail_msg.c_str());
+    msm_job_free(job);
+    return frc;
+  }
   if (job->empty) {
     memset(out, 0, PW * 4);
     msm_job_free(job);
@@ -3486,9 +3502,11 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
     // window sharding (north_star's variant): every rank holds every base and
     // scalar and runs windows [r W / N, (r + 1) W / N) of the plain plan (no
     // fixed-base table: a table folds all windows into one)
-    P.c = ctx->msm_window > 0 ? ctx->msm_window : pick_window(n);
-    if (P.c < 12 || P.c > 22) {
-      set_error("msm_window_sharded: window %d outside 12..22 (zkmi_msm_set_window)", P.c);
+    // (the automatic choice is clamped to >= 12: the window-sharded plan
+    // needs the sort's window filter, which the small-MSM sorts below 12 lack)
+    P.c = ctx->msm_window > 0 ? ctx->msm_window : std::max(12, pick_window(n));
+    if (P.c < 12 || P.c > 17) {
+      set_error("msm_window_sharded: window %d outside 12..17 (zkmi_msm_set_window; 0 = automatic)", P.c);
       rc = ZKMI_EINVAL;
     } else {
       const int Wt = msm_windows(P.c), nr = comm->nranks, r = comm->rank;
@@ -3543,10 +3561,28 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
       rc = msm_queue_handover(ctx, lane, lane->st, job, buf, 0);
   }
   if (rc) {
-    // the peers are in (or heading for) this job's exchange: join it with a
-    // failure status unless this rank's share is already queued (RCCL)
+    // The peers are in (or heading for) this job's exchange: join it with a
+    // failure status.  Over RCCL every exchange is queued on the
+    // communicator's stream in submit order, so the failure exchange goes there
+    // now (unless this rank's share is already queued).  Over a host transport
+    // the exchanges run in msm_wait, in wait order: a failure exchanged here
+    // would pair with the peers' exchange of an earlier job still in flight and
+    // shift every later one, so the job is returned marked failed and
+    // msm_wait exchanges the failure at its turn.
     const std::string err = zkmi_last_error();
-    if (!(job->exchanged && comm->kind == ZKMI_COMM_RCCL)) (void)comm_fail_exchange(comm, SHARD_PAYLOAD_WORDS);
+    if (comm->kind == ZKMI_COMM_HOST) {
+      if (lane) (void)hipStreamSynchronize(lane->st);  // partly queued work: drained before the buffers recycle
+      (void)hipGetLastError();
+      if (job->host) ctx_pinned_put(ctx, job->host);
+      job->host = nullptr;
+      job->st = nullptr;
+      job->fail_rc = rc;
+      job->fail_msg = err;
+      set_error("%s", err.c_str());
+      *out = job;
+      return 0;
+    }
+    if (!job->exchanged) (void)comm_fail_exchange(comm, SHARD_PAYLOAD_WORDS);
     set_error("%s", err.c_str());
     msm_job_free(job);
     return rc;

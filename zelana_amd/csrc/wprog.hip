@@ -42,10 +42,12 @@
 #define ZK_NO_ASM_MAD 1
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "dev_io.h"
 #include "ff.h"
+
 #include "zkmi_internal.h"
 
 namespace zk {
@@ -581,9 +583,29 @@ struct zkmi_wprog {
 };
 
 namespace zk {
+// Release a program's own stream (after its work): called for every program
+// of a context when a communicator is created (stream budget),
+// so the context never holds a fifth stream beside context + 2 lanes + the
+// RCCL stream; later runs go to the context stream (wprog_stream).
+static void wprog_drop_stream(zkmi_wprog* p) {
+  if (!p->st) return;
+  (void)hipStreamSynchronize(p->st);
+  (void)hipStreamDestroy(p->st);
+  p->st = nullptr;
+  p->ctx->nstreams--;
+}
+void wprog_release_streams(zkmi_ctx* ctx) {
+  for (zkmi_wprog* p : ctx->wprogs) wprog_drop_stream(p);
+}
 static void wprog_free(zkmi_wprog* p) {
   if (!p) return;
-  (void)hipStreamSynchronize(p->st ? p->st : p->ctx->stream);  // runs beside a communicator use the context stream
+  // runs may sit on the program's stream and (beside a communicator, or after
+  // its stream was released) on the context stream: both drain before the
+  // buffers go
+  if (p->st) (void)hipStreamSynchronize(p->st);
+  (void)hipStreamSynchronize(p->ctx->stream);
+  auto& reg = p->ctx->wprogs;
+  reg.erase(std::remove(reg.begin(), reg.end(), p), reg.end());
   (void)hipFree(p->d_input_var);
   (void)hipFree(p->d_coeff);
   (void)hipFree(p->d_rc);
@@ -599,10 +621,7 @@ static void wprog_free(zkmi_wprog* p) {
   }
   if (p->done) (void)hipEventDestroy(p->done);
   if (p->ctx_mark) (void)hipEventDestroy(p->ctx_mark);
-  if (p->st) {
-    (void)hipStreamDestroy(p->st);
-    p->ctx->nstreams--;
-  }
+  wprog_drop_stream(p);
   delete p;
 }
 
@@ -613,6 +632,7 @@ static void wprog_free(zkmi_wprog* p) {
 // no fifth stream beside context + 2 lanes + the RCCL stream).
 static int wprog_stream(zkmi_ctx* ctx, zkmi_wprog* p, hipStream_t* st) {
   if (ctx->ncomm > 0) {
+    wprog_drop_stream(p);  // (released at zkmi_comm_init already; kept for safety)
     *st = ctx->stream;
     return 0;
   }
@@ -703,6 +723,7 @@ int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* d, zkmi_wprog** out)
   }
   zkmi_wprog* p = new zkmi_wprog;
   p->ctx = ctx;
+  ctx->wprogs.push_back(p);
   p->num_vars = d->num_vars;
   p->num_inputs = d->num_inputs;
   p->level_start.assign(d->level_start, d->level_start + d->num_levels + 1);

@@ -95,6 +95,7 @@ struct zkmi_ctx {
   // shares a hardware queue with MSM work.
   int ncomm = 0;
   int nstreams = 0;
+  std::vector<zkmi_wprog*> wprogs;  // live witness programs (their streams go when a communicator comes)
 };
 constexpr int MAX_LANES_WITH_COMM = 2;
 
@@ -149,6 +150,8 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
 // with its failure flag set, so the other ranks fail in their msm_wait instead
 // of blocking in the collective.  Synchronous; issue order as the exchange.
 int comm_fail_exchange(zkmi_comm* c, size_t words);
+// release every witness program's own stream (after its work; wprog.hip)
+void wprog_release_streams(zkmi_ctx* ctx);
 // words of the status block that starts every rank's sharded exchange payload
 constexpr size_t SHARD_STATUS_WORDS = 4;
 

@@ -39,21 +39,67 @@ class CommInitError(RuntimeError):
     """libzkmi communicator creation failed on at least one rank."""
 
 
-def make_comm(ctx, backend: str) -> Comm:
-    """libzkmi communicator over the current torch.distributed world:
-    RCCL when the backend is nccl (the unique id is broadcast by rank 0),
-    otherwise the host transport over torch.distributed.
+RCCL_TRANSPORTS = ("rccl", "nccl")
+HOST_TRANSPORTS = ("host", "gloo")
 
-    Every rank reports whether its zkmi_comm_init succeeded (an object
-    all-gather over torch.distributed), so a failure on one rank raises
-    CommInitError with that rank's error text on EVERY rank instead of leaving
-    the others to block in the first collective."""
+
+def transport_from_env() -> str:
+    """libzkmi's exchange transport for this launch: ZKMI_DIST_BACKEND =
+    rccl / nccl (default: RCCL over xGMI, one GPU per rank) or host / gloo
+    (the host transport, to rehearse N ranks on one GPU)."""
+    import os
+
+    t = os.environ.get("ZKMI_DIST_BACKEND", "rccl").lower()
+    if t not in RCCL_TRANSPORTS + HOST_TRANSPORTS:
+        raise ValueError(f"ZKMI_DIST_BACKEND={t!r}: expected one of {RCCL_TRANSPORTS + HOST_TRANSPORTS}")
+    return "rccl" if t in RCCL_TRANSPORTS else "host"
+
+
+def init_world():
+    """torch.distributed for process control only: rendezvous, barriers,
+    timing reductions and the communicator's unique-id broadcast, always over
+    gloo with CPU tensors.  The data path's one collective is libzkmi's own
+    (make_comm), so each rank holds exactly one RCCL communicator and the
+    streams zkmi.h's budget names (context + 2 lanes + the communicator's),
+    never torch's NCCL group and its streams beside them.
+    Returns the torch.distributed module, or None for a 1-rank launch."""
+    import os
+
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None
     import torch.distributed as dist
 
+    if not dist.is_initialized():
+        dist.init_process_group("gloo")
+    return dist
+
+
+def make_comm(ctx, transport: str) -> Comm:
+    """libzkmi communicator over the current torch.distributed (gloo) world:
+    RCCL when transport is "rccl" (rank 0's unique id broadcast over gloo),
+    otherwise the host transport whose all-gather is torch.distributed's.
+
+    A torch NCCL process group is refused: it would be a second RCCL
+    communicator (plus torch's NCCL stream) beside libzkmi's, outside the
+    stream budget.  Every rank reports whether its zkmi_comm_init succeeded
+    (an object all-gather), so a failure on one rank raises CommInitError
+    with that rank's error text on EVERY rank instead of leaving the others to
+    block in the first collective."""
+    import torch.distributed as dist
+
+    if transport in RCCL_TRANSPORTS:
+        transport = "rccl"
+    elif transport in HOST_TRANSPORTS:
+        transport = "host"
+    else:
+        raise ValueError(f"make_comm: unknown transport {transport!r}")
+    if dist.get_backend() != "gloo":
+        raise CommInitError(f"make_comm: torch.distributed runs on {dist.get_backend()!r}; libzkmi's communicator "
+                            "needs a gloo (CPU) process group beside it (init_world), not a second RCCL one")
     world, rank = dist.get_world_size(), dist.get_rank()
     comm, err = None, None
     try:
-        if backend == "nccl":
+        if transport == "rccl":
             obj = [comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             comm = Comm.rccl(ctx, obj[0], world, rank)
@@ -72,18 +118,17 @@ def make_comm(ctx, backend: str) -> Comm:
     return comm
 
 
-def allgather_points(point: np.ndarray, device=None) -> list[np.ndarray]:
-    """All-gather one canonical affine point (8 or 16 u64) from every rank."""
+def allgather_points(point: np.ndarray) -> list[np.ndarray]:
+    """All-gather one canonical affine point (8 or 16 u64) from every rank
+    (CPU tensors: the gloo group of init_world)."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size()
     t = torch.from_numpy(point.view(np.int64).copy())
-    if device is not None:
-        t = t.to(device)
     bufs = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(bufs, t)
-    return [b.cpu().numpy().view(np.uint64) for b in bufs]
+    return [b.numpy().view(np.uint64) for b in bufs]
 
 
 def sum_points(points: list[np.ndarray]) -> np.ndarray:
@@ -94,6 +139,6 @@ def sum_points(points: list[np.ndarray]) -> np.ndarray:
     return acc
 
 
-def combine_partials(point: np.ndarray, device=None) -> np.ndarray:
+def combine_partials(point: np.ndarray) -> np.ndarray:
     """Global MSM result from this rank's partial (identical on every rank)."""
-    return sum_points(allgather_points(point, device))
+    return sum_points(allgather_points(point))

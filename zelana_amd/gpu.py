@@ -367,7 +367,7 @@ class ProvingKey:
     def __init__(self, ctx: Context, pk_bytes: bytes, compressed: bool = True):
         self.ctx = ctx
         self.h = vp()
-        buf = np.frombuffer(pk_bytes, np.uint8).copy()
+        buf = np.frombuffer(pk_bytes, np.uint8)  # (read only: zkmi_pk_load takes a const pointer; no host copy)
         check(lib().zkmi_pk_load(ctx.h, buf.ctypes.data_as(u8p), len(pk_bytes), int(compressed),
                                  ctypes.byref(self.h)), "zkmi_pk_load")
         info = np.zeros(3, np.uint64)
