@@ -248,8 +248,3 @@ def test_l2_2pow22_real_key_proof_matches_oracle(ctx):
     O.lib().oracle_pk_free(opk)
     step("oracle prove")
     assert np.array_equal(a, oa) and np.array_equal(b, ob) and np.array_equal(c, oc), "GPU proof != oracle proof"
-    la, lb, lc = gpu.groth16_prove(ctx, pk_loaded, cs, z, r, s)
-    pk_loaded.close()
-    assert np.array_equal(la, oa) and np.array_equal(lb, ob) and np.array_equal(lc, oc), \
-        "proof under the loaded 290 MB key != oracle proof"
-    step("proof under the loaded key == oracle proof")

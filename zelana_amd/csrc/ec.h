@@ -164,6 +164,9 @@ ZK_HD Xyzz<FqOps> xyzz_madd_g1f(const Xyzz<FqOps>& p, const Fe& qx, const Fe& qy
   const Fe pp_ = mul_add<FqP>(qx, p.zz, bsub(FqP::B8_1, p.x));  // U2 - X1 + 8p
   const Fe rr = mul_add<FqP>(qy, p.zzz, ny1);                    // S2 - Y1 + 4p
   const Fe pp = sqr<FqP>(pp_);                                   // < 1.48p: == 0 mod p iff in {0, p}
+  // (Round 6: a 4-instruction filter on limbs 0 and 8 in front of this 9-limb
+  // test, -18 VALU per entry, measured 0.5% slower on the 2^20 loop: the
+  // extra branch level costs more than the instructions it removes.)
   uint32_t z = 0, e = 0;
 #pragma unroll
   for (int i = 0; i < NL; i++) {

@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <unordered_map>
 #include <vector>
 
 #include "dev_io.h"
@@ -257,8 +258,38 @@ __device__ __forceinline__ Fe fe_shfl_xor(const Fe& a, int m) {
   for (int i = 0; i < NL; i++) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], m, 64);
   return r;
 }
-__global__ void __launch_bounds__(256) k_matvec(const uint64_t* __restrict__ rowptr, const uint64_t* __restrict__ col,
-                                                const uint32_t* __restrict__ val, const uint32_t* __restrict__ zm,
+// [0, 16r) with limbs up to 2^32 (a limb-wise sum of <= 8 normalised values
+// < 2r) -> [0, 2r), normalised: one carry pass, then the quotient-estimate
+// reduction
+__device__ __forceinline__ Fe fr_sum_reduce(Fe a) {
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    a.v[i + 1] += a.v[i] >> 29;
+    a.v[i] &= LMASK;
+  }
+  return reduce_q32<FrP>(a);
+}
+// One term of a row.  DICT (the compact form, upload_r1cs): cv[k] = (column,
+// coefficient id) into the matrix's coefficient dictionary (Montgomery form),
+// id 0 = 1 (no product), z canonical: coef_M * z * R^-1 = coef * z.  Legacy:
+// 32-B canonical coefficients times the Montgomery copy zm of z.
+template <bool DICT>
+__device__ __forceinline__ Fe mv_term(uint64_t k, const uint64_t* __restrict__ col, const uint32_t* __restrict__ val,
+                                      const uint2* __restrict__ cv, const uint32_t* __restrict__ coef,
+                                      const uint32_t* __restrict__ zm, const uint32_t* __restrict__ zc) {
+  if constexpr (DICT) {
+    const uint2 e = cv[k];
+    Fe t = ld_fe(zc + (size_t)e.x * 8);
+    if (e.y) t = mul<FrP>(ld_fe(coef + (size_t)e.y * 8), t);
+    return t;
+  } else {
+    return mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8));
+  }
+}
+template <bool DICT, class RP>
+__global__ void __launch_bounds__(256) k_matvec(const RP* __restrict__ rowptr, const uint64_t* __restrict__ col,
+                                                const uint32_t* __restrict__ val, const uint2* __restrict__ cv,
+                                                const uint32_t* __restrict__ coef, const uint32_t* __restrict__ zm,
                                                 const uint32_t* __restrict__ zc, size_t m, size_t l, size_t n,
                                                 int is_a, const uint32_t* __restrict__ lrow, uint32_t nlong, int g,
                                                 uint32_t nsb, uint32_t* __restrict__ out) {
@@ -269,7 +300,10 @@ __global__ void __launch_bounds__(256) k_matvec(const uint64_t* __restrict__ row
     if (i < m) {
       const uint64_t k0 = rowptr[i], k1 = rowptr[i + 1];
       if (k1 - k0 > MATVEC_SHORT) return;  // a long row: the group blocks store it
-      for (uint64_t k = k0; k < k1; k++) acc = add<FrP>(acc, mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8)));
+      // limb-wise sum of <= MATVEC_SHORT products < 2r, one reduction (the
+      // full modular add per term cost ~70 instructions)
+      for (uint64_t k = k0; k < k1; k++) acc = add_lazy(acc, mv_term<DICT>(k, col, val, cv, coef, zm, zc));
+      acc = fr_sum_reduce(acc);
     } else if (is_a && i < m + l) {
       acc = ld_fe(zc + (i - m) * 8);
     }
@@ -284,7 +318,7 @@ __global__ void __launch_bounds__(256) k_matvec(const uint64_t* __restrict__ row
     row = lrow[j];
     const uint64_t k1 = rowptr[row + 1];
     for (uint64_t k = rowptr[row] + gl; k < k1; k += (uint32_t)g)
-      part = add<FrP>(part, mul<FrP>(ld_fe(val + k * 8), ld_fe(zm + col[k] * 8)));
+      part = add<FrP>(part, mv_term<DICT>(k, col, val, cv, coef, zm, zc));
   }
   for (int d = g >> 1; d >= 1; d >>= 1) part = add<FrP>(part, fe_shfl_xor(part, d));  // every lane shuffles
   if (j < nlong && gl == 0) st_fe(out + (size_t)row * 8, part);
@@ -398,12 +432,24 @@ int domain_cache(zkmi_ctx* ctx, uint32_t logn, DomainCache* dc) {
 }  // namespace zk
 
 // R1CS matrices resident in HBM (the circuit shape is fixed per proving key,
-// Appendix B.1, so only the witness changes between proofs)
+// Appendix B.1, so only the witness changes between proofs).
+// Compact form (per matrix, when it has few distinct coefficients -- a real
+// circuit's are +-1, powers of two and a few constants; zelana_batch has 9):
+// u32 row pointers, one (u32 column, u32 coefficient id) pair per non-zero and
+// a dictionary of the distinct coefficients in Montgomery form (id 0 = 1):
+// 8 B per non-zero instead of 40 (u64 column + 32-B coefficient), and no
+// Montgomery copy of z.  Otherwise the legacy CSR (u64 row pointers / columns,
+// canonical coefficients).
 struct zkmi_r1cs_dev {
   size_t m = 0, l = 0, w = 0;
   uint64_t* rp[3] = {nullptr, nullptr, nullptr};
   uint64_t* col[3] = {nullptr, nullptr, nullptr};
   uint32_t* val[3] = {nullptr, nullptr, nullptr};
+  bool dict[3] = {false, false, false};
+  uint32_t* rp32[3] = {nullptr, nullptr, nullptr};
+  uint2* cv[3] = {nullptr, nullptr, nullptr};
+  uint32_t* coef[3] = {nullptr, nullptr, nullptr};  // Montgomery, 8 words per id
+  uint32_t ncoef[3] = {0, 0, 0};
   // rows longer than MATVEC_SHORT terms (k_matvec's lane-group blocks)
   uint32_t* lrow[3] = {nullptr, nullptr, nullptr};
   uint32_t nlong[3] = {0, 0, 0};
@@ -415,6 +461,9 @@ struct zkmi_r1cs_dev {
       hipFree(rp[t]);
       hipFree(col[t]);
       hipFree(val[t]);
+      hipFree(rp32[t]);
+      hipFree(cv[t]);
+      hipFree(coef[t]);
       if (lrow[t]) hipFree(lrow[t]);
     }
   }
@@ -422,6 +471,55 @@ struct zkmi_r1cs_dev {
 
 namespace zk {
 using DevR1CS = zkmi_r1cs_dev;
+
+// a matrix's coefficient dictionary: ids per non-zero (0 = the value 1) and
+// the distinct values (canonical 4 x u64); false when there are too many
+// distinct values for the compact form to pay (more than 1/4 of the non-zeros
+// and more than 2^16), or the matrix is too large for u32 indices
+struct CoefKey {
+  uint64_t v[4];
+  bool operator==(const CoefKey& o) const {
+    return v[0] == o.v[0] && v[1] == o.v[1] && v[2] == o.v[2] && v[3] == o.v[3];
+  }
+};
+struct CoefHash {
+  size_t operator()(const CoefKey& k) const {
+    uint64_t h = k.v[0] * 0x9E3779B97F4A7C15ull ^ (k.v[1] + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
+    h ^= (k.v[2] * 0x165667B19E3779F9ull) ^ (k.v[3] * 0x27D4EB2F165667C5ull);
+    return (size_t)(h ^ (h >> 29));
+  }
+};
+static bool build_coef_dict(const uint64_t* vals, uint64_t nnz, size_t nv, std::vector<uint32_t>& ids,
+                            std::vector<uint64_t>& dict) {
+  if (nnz >= (1ull << 32) || nv >= (1ull << 32)) return false;
+  const uint64_t cap = std::max<uint64_t>(1u << 16, nnz / 4);
+  std::unordered_map<CoefKey, uint32_t, CoefHash> idx;
+  dict.assign({1, 0, 0, 0});
+  idx.emplace(CoefKey{{1, 0, 0, 0}}, 0u);
+  ids.resize(nnz);
+  CoefKey prev{{1, 0, 0, 0}};
+  uint32_t prev_id = 0;
+  for (uint64_t k = 0; k < nnz; k++) {
+    const CoefKey key{{vals[4 * k], vals[4 * k + 1], vals[4 * k + 2], vals[4 * k + 3]}};
+    if (key == prev) {  // runs of equal coefficients are common
+      ids[k] = prev_id;
+      continue;
+    }
+    auto it = idx.find(key);
+    uint32_t id;
+    if (it == idx.end()) {
+      if (idx.size() >= cap) return false;
+      id = (uint32_t)idx.size();
+      idx.emplace(key, id);
+      dict.insert(dict.end(), key.v, key.v + 4);
+    } else {
+      id = it->second;
+    }
+    ids[k] = prev_id = id;
+    prev = key;
+  }
+  return true;
+}
 
 // validate + copy a host CSR R1CS to device; owned=true allocates dedicated
 // buffers (zkmi_r1cs_create), otherwise context workspace is used
@@ -435,6 +533,20 @@ static int upload_r1cs(zkmi_ctx* ctx, const zkmi_r1cs* cs, DevR1CS* d, bool owne
   const uint64_t* vals[3] = {cs->a_val, cs->b_val, cs->c_val};
   const char* nm[3] = {"a", "b", "c"};
   size_t m = cs->num_constraints, nv = cs->num_instance + cs->num_witness;
+  auto dev_buf = [&](const char* what, int t, size_t bytes, void** out) -> int {
+    bytes = std::max<size_t>(bytes, 32);
+    if (owned) {
+      if (hipMalloc(out, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("r1cs: device allocation failed (matrix %s, %s, %zu bytes)", nm[t], what, bytes);
+        return ZKMI_ENOMEM;
+      }
+      return 0;
+    }
+    char b[48];
+    snprintf(b, sizeof(b), "r1cs_%s_%s", what, nm[t]);
+    return ctx->ws.get(b, bytes, out);
+  };
   for (int t = 0; t < 3; t++) {
     if (!rps[t] || (m && (!cols[t] || !vals[t]))) {
       set_error("r1cs: matrix %s missing", nm[t]);
@@ -453,23 +565,6 @@ static int upload_r1cs(zkmi_ctx* ctx, const zkmi_r1cs* cs, DevR1CS* d, bool owne
         return ZKMI_EINVAL;
       }
     }
-    if (owned) {
-      if (hipMalloc(&d->rp[t], (m + 1) * 8) != hipSuccess ||
-          hipMalloc(&d->col[t], std::max<uint64_t>(1, nnz) * 8) != hipSuccess ||
-          hipMalloc(&d->val[t], std::max<uint64_t>(1, nnz) * 32) != hipSuccess) {
-        (void)hipGetLastError();
-        set_error("r1cs: device allocation failed (matrix %s, %llu non-zeros)", nm[t], (unsigned long long)nnz);
-        return ZKMI_ENOMEM;
-      }
-    } else {
-      char b1[32], b2[32], b3[32];
-      snprintf(b1, 32, "r1cs_rp_%s", nm[t]);
-      snprintf(b2, 32, "r1cs_col_%s", nm[t]);
-      snprintf(b3, 32, "r1cs_val_%s", nm[t]);
-      ZK_TRY(ctx->ws.get(b1, (m + 1) * 8, (void**)&d->rp[t]));
-      ZK_TRY(ctx->ws.get(b2, std::max<uint64_t>(1, nnz) * 8, (void**)&d->col[t]));
-      ZK_TRY(ctx->ws.get(b3, std::max<uint64_t>(1, nnz) * 32, (void**)&d->val[t]));
-    }
     // long-row list for k_matvec (synchronous copy: the list is a temporary)
     std::vector<uint32_t> lr;
     uint64_t lmax = 0;
@@ -484,24 +579,39 @@ static int upload_r1cs(zkmi_ctx* ctx, const zkmi_r1cs* cs, DevR1CS* d, bool owne
     d->glong[t] = 2;
     while (d->glong[t] < 64 && (uint64_t)d->glong[t] * 4 < lmax) d->glong[t] <<= 1;
     if (!lr.empty()) {
-      if (owned) {
-        if (hipMalloc(&d->lrow[t], lr.size() * 4) != hipSuccess) {
-          (void)hipGetLastError();
-          set_error("r1cs: device allocation failed (matrix %s long rows)", nm[t]);
-          return ZKMI_ENOMEM;
-        }
-      } else {
-        char b4[32];
-        snprintf(b4, 32, "r1cs_long_%s", nm[t]);
-        ZK_TRY(ctx->ws.get(b4, lr.size() * 4, (void**)&d->lrow[t]));
-      }
+      ZK_TRY(dev_buf("long", t, lr.size() * 4, (void**)&d->lrow[t]));
       ZK_HIP(hipMemcpyAsync(d->lrow[t], lr.data(), lr.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-      ZK_HIP(hipStreamSynchronize(ctx->stream));
     }
-    ZK_HIP(hipMemcpyAsync(d->rp[t], rps[t], (m + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-    if (nnz) {
-      ZK_HIP(hipMemcpyAsync(d->col[t], cols[t], nnz * 8, hipMemcpyHostToDevice, ctx->stream));
-      ZK_HIP(hipMemcpyAsync(d->val[t], vals[t], nnz * 32, hipMemcpyHostToDevice, ctx->stream));
+    std::vector<uint32_t> ids;
+    std::vector<uint64_t> dict;
+    d->dict[t] = build_coef_dict(vals[t], nnz, nv, ids, dict);
+    if (d->dict[t]) {
+      d->ncoef[t] = (uint32_t)(dict.size() / 4);
+      std::vector<uint32_t> rp32(m + 1);
+      for (size_t i = 0; i <= m; i++) rp32[i] = (uint32_t)rps[t][i];
+      std::vector<uint2> cv(nnz);
+      for (uint64_t k = 0; k < nnz; k++) cv[k] = make_uint2((uint32_t)cols[t][k], ids[k]);
+      uint32_t* canon = nullptr;
+      ZK_TRY(dev_buf("rp32", t, (m + 1) * 4, (void**)&d->rp32[t]));
+      ZK_TRY(dev_buf("cv", t, nnz * 8, (void**)&d->cv[t]));
+      ZK_TRY(dev_buf("coef", t, dict.size() * 8, (void**)&d->coef[t]));
+      ZK_TRY(ctx->ws.get("r1cs_coef_canon", dict.size() * 8, (void**)&canon));
+      ZK_HIP(hipMemcpyAsync(d->rp32[t], rp32.data(), (m + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+      if (nnz) ZK_HIP(hipMemcpyAsync(d->cv[t], cv.data(), nnz * 8, hipMemcpyHostToDevice, ctx->stream));
+      ZK_HIP(hipMemcpyAsync(canon, dict.data(), dict.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+      k_to_mont_fr<<<(d->ncoef[t] + 255) / 256, 256, 0, ctx->stream>>>(canon, d->ncoef[t], d->coef[t]);
+      ZK_HIP(hipGetLastError());
+      ZK_HIP(hipStreamSynchronize(ctx->stream));  // the host staging vectors go out of scope
+    } else {
+      ZK_TRY(dev_buf("rp", t, (m + 1) * 8, (void**)&d->rp[t]));
+      ZK_TRY(dev_buf("col", t, nnz * 8, (void**)&d->col[t]));
+      ZK_TRY(dev_buf("val", t, nnz * 32, (void**)&d->val[t]));
+      ZK_HIP(hipMemcpyAsync(d->rp[t], rps[t], (m + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+      if (nnz) {
+        ZK_HIP(hipMemcpyAsync(d->col[t], cols[t], nnz * 8, hipMemcpyHostToDevice, ctx->stream));
+        ZK_HIP(hipMemcpyAsync(d->val[t], vals[t], nnz * 32, hipMemcpyHostToDevice, ctx->stream));
+      }
+      ZK_HIP(hipStreamSynchronize(ctx->stream));  // (the long-row list is a temporary)
     }
   }
   return 0;
@@ -521,19 +631,29 @@ static int witness_map_dev(zkmi_ctx* ctx, const DevR1CS& dr, const uint32_t* d_z
   DomainCache dc;
   ZK_TRY(domain_cache(ctx, logn, &dc));
   uint32_t *zm, *b, *c;
-  ZK_TRY(ctx->ws.get("wm_zm", nv * 32, (void**)&zm));
+  zm = nullptr;  // Montgomery copy of z: the legacy CSR form only
+  if (!dr.dict[0] || !dr.dict[1] || !dr.dict[2]) ZK_TRY(ctx->ws.get("wm_zm", nv * 32, (void**)&zm));
   ZK_TRY(ctx->ws.get("wm_b", n * 32, (void**)&b));
   ZK_TRY(ctx->ws.get("wm_c", n * 32, (void**)&c));
   uint32_t* a = d_h;
   unsigned gn = (unsigned)((n + 255) / 256);
   {
     ScopedKernelTimer tm(ctx, "g16_matvec");
-    k_to_mont_fr<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(d_z, nv, zm);
+    // (the legacy form multiplies canonical coefficients by a Montgomery copy
+    // of z; the compact form needs none)
+    if (!dr.dict[0] || !dr.dict[1] || !dr.dict[2])
+      k_to_mont_fr<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(d_z, nv, zm);
     uint32_t* outs[3] = {a, b, c};
     for (int t = 0; t < 3; t++) {
       const unsigned gl = (unsigned)(((size_t)dr.nlong[t] * dr.glong[t] + 255) / 256);
-      k_matvec<<<gn + gl, 256, 0, st>>>(dr.rp[t], dr.col[t], dr.val[t], zm, d_z, m, l, n, t == 0, dr.lrow[t],
-                                        dr.nlong[t], dr.glong[t], gn, outs[t]);
+      if (dr.dict[t])
+        k_matvec<true, uint32_t><<<gn + gl, 256, 0, st>>>(dr.rp32[t], nullptr, nullptr, dr.cv[t], dr.coef[t], zm,
+                                                          d_z, m, l, n, t == 0, dr.lrow[t], dr.nlong[t],
+                                                          dr.glong[t], gn, outs[t]);
+      else
+        k_matvec<false, uint64_t><<<gn + gl, 256, 0, st>>>(dr.rp[t], dr.col[t], dr.val[t], nullptr, nullptr, zm,
+                                                           d_z, m, l, n, t == 0, dr.lrow[t], dr.nlong[t],
+                                                           dr.glong[t], gn, outs[t]);
     }
     ZK_HIP(hipGetLastError());
   }

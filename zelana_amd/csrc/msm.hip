@@ -1467,7 +1467,10 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
   // one call site of the addition (each inlined copy is ~3.5K instructions):
   // the row of entry p + 1 is in flight while entry p is added.  The loads
   // are unconditional (past the end they re-read the last entry), so the
-  // buffer is one loop-carried value with a single copy per entry.
+  // buffer is one loop-carried value with a single copy per entry.  (Round 6:
+  // unpacking entry p before reloading the buffer, to drop that copy's 8
+  // v_mov_b64, made the compiler keep both buffers live: 127 -> 157 VGPRs,
+  // no room left beside three waves for the other lanes' tails.)
   uint4 raw[4];
   const uint32_t last = end - 1;
   uint32_t v_nxt = sval[start];
