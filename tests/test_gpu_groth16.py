@@ -132,6 +132,42 @@ def test_synthetic_prove_and_witness_map(ctx, m, l, w, sat):
     O.lib().oracle_pk_free(opk)
 
 
+def test_witness_map_compact_and_legacy_matrices(ctx):
+    """Both R1CS forms of the witness map's mat-vecs (groth16.hip
+    upload_r1cs): A has ~100 K distinct random coefficients (above the
+    dictionary cap: legacy 40-B CSR), B and C draw their coefficients from 7
+    values including 1 (compact form: u32 column + coefficient id, id 0 = no
+    product); every matrix has short rows (one lane, lazy sum) and long rows
+    of 9-70 terms (lane groups).  h equals the oracle's."""
+    from zelana_amd import gpu
+    from zelana_amd.r1cs import R1CS, _rand_fr_array
+    rng = np.random.default_rng(61)
+    m, l, w = 33000, 5, 33100
+    nv = l + w
+    cs = R1CS(l, w)
+    pool = _rand_fr_array(rng, 7)
+    pool[0] = [1, 0, 0, 0]
+    for name in ("a", "b", "c"):
+        lens = rng.integers(1, 5, size=m)
+        lens[rng.choice(m, 300, replace=False)] = rng.integers(9, 71, size=300)
+        rp = np.zeros(m + 1, np.uint64)
+        rp[1:] = np.cumsum(lens)
+        nnz = int(rp[-1])
+        col = rng.integers(0, nv, size=nnz, dtype=np.uint64)
+        val = _rand_fr_array(rng, nnz) if name == "a" else pool[rng.integers(0, 7, size=nnz)]
+        cs.set_csr(name, rp, col, val)
+    cs._m = m
+    z = _rand_fr_array(rng, nv)
+    z[0] = [1, 0, 0, 0]
+    st, keep = O.make_r1cs(cs)
+    n = 1
+    while n < m + l:
+        n <<= 1
+    h_ref = np.zeros((n, 4), np.uint64)
+    O.lib().oracle_witness_map(ctypes.byref(st), O.P(z), O.P(h_ref), 8)
+    assert np.array_equal(gpu.witness_map(ctx, cs, z), h_ref)
+
+
 def test_pk_load_rejects_bad_points(ctx):
     from zelana_amd import ZkmiError, gpu
     cs, z = square_circuit(7)

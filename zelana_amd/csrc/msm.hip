@@ -2850,7 +2850,10 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
   lane->debug_sorted = 1;
   ScopedKernelTimer tm(ctx, "msm_sort", st);
   if (fused && !small) {
-    // bin sort (k_bs_*): memset + 4 kernels; items for one-lane-per-bucket plans
+    // bin sort (k_bs_*): five kernels (count, scatter1, count2, scatter2 and,
+    // for one-lane-per-bucket plans, the item placement); the counter blocks
+    // are cleared by the previous sort's count kernel, so a memset runs only
+    // when the blocks are new or a sort was interrupted
     const BsGeom g = bs_geom(P, n);
     const bool items = items_plan(P);
     uint32_t *ctr2, *choff, *thist;

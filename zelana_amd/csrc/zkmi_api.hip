@@ -154,7 +154,22 @@ int zkmi_ctx_create(int device, zkmi_ctx** out) {
   zkmi_ctx* c = new zkmi_ctx;
   c->device = device;
   c->num_cus = prop.multiProcessorCount;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  // The context stream carries a proof's witness map (mat-vecs, 7 NTTs, the
+  // QAP step), the critical path to the h MSM, while the lanes run the
+  // z-weighted MSMs beside it.  The G2 accumulation holds 248 VGPRs, two
+  // waves per SIMD, so an NTT wave gets a SIMD only when an accumulation wave
+  // retires; at the highest queue priority the dispatcher hands it that slot
+  // first (round 6 trace: NTT passes of 2.4-4.1 ms beside the G2 accumulation
+  // against ~0.2 ms alone).  Measured (tools/r06_ab2.sh, 2 repeats): 2^22
+  // proofs 33.3-33.4 -> 34.0/s, two in flight 33.7 -> 34.6-35.0/s; batch 70
+  // resident 81.5-81.6 -> 82.2-82.3/s, end to end (4 per witness run)
+  // 78.8-78.9 -> 80.3-81.0/s.
+#ifndef ZK_CTX_PRIO
+#define ZK_CTX_PRIO 1
+#endif
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, ZK_CTX_PRIO ? prio_hi : prio_lo) != hipSuccess) {
     delete c;
     set_error("hipStreamCreate failed");
     return ZKMI_EHIP;
