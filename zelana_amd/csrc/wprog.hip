@@ -561,7 +561,8 @@ __global__ void __launch_bounds__(256) k_wprog_to_mont(uint32_t* __restrict__ v,
 }  // namespace zk
 
 struct zkmi_wprog {
-  zkmi_ctx* ctx = nullptr;
+  zkmi_ctx* ctx = nullptr;  // null once the context is destroyed (wprog_detach_all): the program is then only freed
+  int device = 0;
   size_t num_vars = 0, num_inputs = 0;
   uint32_t *d_input_var = nullptr, *d_coeff = nullptr, *d_rc = nullptr, *d_in = nullptr;
   uint4* d_ops = nullptr;
@@ -592,10 +593,21 @@ static void wprog_drop_stream(zkmi_wprog* p) {
   (void)hipStreamSynchronize(p->st);
   (void)hipStreamDestroy(p->st);
   p->st = nullptr;
-  p->ctx->nstreams--;
+  if (p->ctx) p->ctx->nstreams--;
 }
 void wprog_release_streams(zkmi_ctx* ctx) {
   for (zkmi_wprog* p : ctx->wprogs) wprog_drop_stream(p);
+}
+// zkmi_ctx_destroy with programs still alive (a caller may free its context
+// before its programs, e.g. a garbage collector's order): their streams go
+// with the context and they forget it, so a later zkmi_wprog_destroy only
+// frees the program's own buffers (on its device).
+void wprog_detach_all(zkmi_ctx* ctx) {
+  for (zkmi_wprog* p : ctx->wprogs) {
+    wprog_drop_stream(p);
+    p->ctx = nullptr;
+  }
+  ctx->wprogs.clear();
 }
 static void wprog_free(zkmi_wprog* p) {
   if (!p) return;
@@ -603,9 +615,11 @@ static void wprog_free(zkmi_wprog* p) {
   // its stream was released) on the context stream: both drain before the
   // buffers go
   if (p->st) (void)hipStreamSynchronize(p->st);
-  (void)hipStreamSynchronize(p->ctx->stream);
-  auto& reg = p->ctx->wprogs;
-  reg.erase(std::remove(reg.begin(), reg.end(), p), reg.end());
+  if (p->ctx) {
+    (void)hipStreamSynchronize(p->ctx->stream);
+    auto& reg = p->ctx->wprogs;
+    reg.erase(std::remove(reg.begin(), reg.end(), p), reg.end());
+  }
   (void)hipFree(p->d_input_var);
   (void)hipFree(p->d_coeff);
   (void)hipFree(p->d_rc);
@@ -723,6 +737,7 @@ int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* d, zkmi_wprog** out)
   }
   zkmi_wprog* p = new zkmi_wprog;
   p->ctx = ctx;
+  p->device = ctx->device;
   ctx->wprogs.push_back(p);
   p->num_vars = d->num_vars;
   p->num_inputs = d->num_inputs;
@@ -803,7 +818,7 @@ int zkmi_wprog_create(zkmi_ctx* ctx, const zkmi_wprog_desc* d, zkmi_wprog** out)
 
 void zkmi_wprog_destroy(zkmi_wprog* p) {
   if (!p) return;
-  ZK_DEVICE_GUARD(p->ctx);
+  ::zk::DeviceGuard guard(p->device);  // (the context may be gone: wprog_detach_all)
   wprog_free(p);
 }
 

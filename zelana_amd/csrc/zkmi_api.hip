@@ -183,6 +183,7 @@ void zkmi_ctx_destroy(zkmi_ctx* ctx) {
   ZK_DEVICE_GUARD(ctx);
   ctx_sync_all(ctx);
   timer_flush(ctx);
+  wprog_detach_all(ctx);
   ctx->ws.release_all();
   for (auto* l : ctx->lanes) {
     l->ws.release_all();

@@ -152,6 +152,8 @@ int msm_submit_sharded(zkmi_comm* comm, const zkmi_bases* b, size_t offset, cons
 int comm_fail_exchange(zkmi_comm* c, size_t words);
 // release every witness program's own stream (after its work; wprog.hip)
 void wprog_release_streams(zkmi_ctx* ctx);
+// the context is being destroyed: its programs drop their streams and forget it
+void wprog_detach_all(zkmi_ctx* ctx);
 // words of the status block that starts every rank's sharded exchange payload
 constexpr size_t SHARD_STATUS_WORDS = 4;
 

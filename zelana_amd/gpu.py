@@ -6,6 +6,7 @@ ABI.  One Context per GPU (one process per GPU, see bench.py).
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import numpy as np
 
@@ -64,6 +65,7 @@ class DeviceView(DeviceBuffer):
 
 class Bases:
     def __init__(self, ctx: "Context", points, g2: bool, *, generate_seed=None, n=None, first=0):
+        ctx._track(self)
         if generate_seed is not None:
             self.ctx, self.g2, self.n = ctx, g2, n
             self.h = vp()
@@ -98,11 +100,14 @@ class Bases:
         check(lib().zkmi_bases_export(self.h, _p64(out)), "zkmi_bases_export")
         return out
 
+    def close(self):
+        if self.h:
+            lib().zkmi_bases_destroy(self.h)
+            self.h = vp()
+
     def __del__(self):
         try:
-            if self.h:
-                lib().zkmi_bases_destroy(self.h)
-                self.h = vp()
+            self.close()
         except Exception:
             pass
 
@@ -111,10 +116,23 @@ class Context:
     def __init__(self, device: int = 0):
         self.h = vp()
         self.device = device
+        # native objects made on this context (base sets, keys, R1CS, witness
+        # programs, communicators): close() frees them first, so none outlives
+        # the context it points to whatever order the garbage collector picks
+        self._deps = weakref.WeakSet()
         check(lib().zkmi_ctx_create(device, ctypes.byref(self.h)), "zkmi_ctx_create")
+
+    def _track(self, obj):
+        self._deps.add(obj)
+        return obj
 
     def close(self):
         if self.h:
+            for obj in list(self._deps):
+                try:
+                    obj.close()
+                except Exception:
+                    pass
             lib().zkmi_ctx_destroy(self.h)
             self.h = vp()
 
@@ -171,6 +189,7 @@ class Context:
         point stream; P0, D canonical affine, 8 u64 each)."""
         b = Bases.__new__(Bases)
         b.ctx, b.g2, b.n, b.h = self, False, n, vp()
+        self._track(b)
         p0 = np.ascontiguousarray(p0, np.uint64)
         d = np.ascontiguousarray(d, np.uint64)
         check(lib().zkmi_bases_generate_arith_g1(self.h, _p64(p0), _p64(d), first, n, ctypes.byref(b.h)),
@@ -265,6 +284,7 @@ class Comm:
         self.ctx = ctx
         self.h = vp()
         self._cb = None
+        ctx._track(self)
 
     @classmethod
     def rccl(cls, ctx: Context, uid: bytes, nranks: int, rank: int) -> "Comm":
@@ -367,6 +387,7 @@ class ProvingKey:
     def __init__(self, ctx: Context, pk_bytes: bytes, compressed: bool = True):
         self.ctx = ctx
         self.h = vp()
+        ctx._track(self)
         buf = np.frombuffer(pk_bytes, np.uint8)  # (read only: zkmi_pk_load takes a const pointer; no host copy)
         check(lib().zkmi_pk_load(ctx.h, buf.ctypes.data_as(u8p), len(pk_bytes), int(compressed),
                                  ctypes.byref(self.h)), "zkmi_pk_load")
@@ -411,6 +432,7 @@ class ProvingKey:
         pk = cls.__new__(cls)
         pk.ctx = ctx
         pk.h = vp()
+        ctx._track(pk)
         check(lib().zkmi_groth16_setup(ctx.h, ctypes.byref(st), _p64(tw), _p64(np.ascontiguousarray(g1, np.uint64)),
                                        _p64(np.ascontiguousarray(g2, np.uint64)), ctypes.byref(pk.h)),
               "zkmi_groth16_setup")
@@ -517,6 +539,7 @@ class R1CSDevice:
         self.ctx = ctx
         st, keep = r1cs_struct(cs)
         self.h = vp()
+        ctx._track(self)
         check(lib().zkmi_r1cs_create(ctx.h, ctypes.byref(st), ctypes.byref(self.h)), "zkmi_r1cs_create")
         self.num_variables = cs.num_instance + cs.num_witness
         del keep

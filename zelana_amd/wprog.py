@@ -162,6 +162,8 @@ class WitnessProgram:
 
     def __init__(self, ctx, plan: Plan):
         self.ctx, self.plan = ctx, plan
+        self.h = vp()
+        ctx._track(self)
         d = WprogDesc()
         d.num_vars = plan.num_vars
         d.num_inputs = plan.input_var.size
