@@ -59,6 +59,10 @@ int zkmi_version(void);
 
 /* ------------------------------------------------------------- context */
 int zkmi_ctx_create(int device, zkmi_ctx** out);
+/* Destroy the objects made on a context (base sets, keys, device R1CS,
+ * communicators, MSM jobs) before the context.  Witness programs may outlive
+ * it: zkmi_ctx_destroy detaches them, and zkmi_wprog_destroy then only frees
+ * their buffers. */
 void zkmi_ctx_destroy(zkmi_ctx* ctx);
 /* per-kernel timing with HIP events on the context's stream (bench/profiling) */
 int zkmi_profile_enable(zkmi_ctx* ctx, int on);
