@@ -160,9 +160,14 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint3
     const uint32_t lhl = lo + rb - g.lsub;  // j-bit of the pair distance
     const uint32_t sh = g.logn - (g.colbits + lhl + 1);
     const uint64_t half = 1ull << (g.logn - 1);
-    Fe w[NP];  // twiddles (unpacked planes)
+    // twiddles (unpacked planes).  The twiddle of pair p depends only on the
+    // bits of p below rb (the higher ones select slot bits above the pair
+    // distance), so a stage loads 2^rb of them, not NP: 3 instead of 4 per
+    // radix-4 round.
+    Fe w[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) {
+      if (p >= (1 << rb)) continue;
       if (TRIV && (p & ((1 << rb) - 1)) == 0) continue;
       const int t0 = ((p >> rb) << (rb + 1)) | (p & ((1 << rb) - 1));
       const uint32_t e0 = base | ((uint32_t)t0 << lo);
@@ -202,7 +207,7 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint3
           continue;
         }
         if (lb[t1] > 2) v = fr_norm(v);  // product operand limbs < 2^30
-        const Fe t = mul<FrP>(v, w[p]);
+        const Fe t = mul<FrP>(v, w[p & ((1 << rb) - 1)]);
         x[t1] = subk<FrP, 2>(u, t);
         bd[t1] = bd[t0] + 2;
         lb[t1] = 1;
@@ -228,7 +233,7 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint3
         x[t0] = sum;
         bd[t0] = bu + bd[t1];
         lb[t0] = ls;
-        x[t1] = one_w ? dlt : mul<FrP>(dlt, w[p]);
+        x[t1] = one_w ? dlt : mul<FrP>(dlt, w[p & ((1 << rb) - 1)]);
         bd[t1] = one_w ? bu + bv : 2;
         lb[t1] = 1;
       }
