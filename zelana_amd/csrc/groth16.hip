@@ -1063,8 +1063,43 @@ int groth16_prove_submit(zkmi_ctx* ctx, const zkmi_pk* pk, const DevR1CS& dr, co
   zkmi_msm_job** jobs = pj->jobs;
   for (int i = 0; i < 5; i++) jobs[i] = nullptr;
   int rc = 0;
+// 1: large-proof schedule below (measured, 2^22 L2 proofs 34.7-34.8 ->
+// 36.1-36.2/s, two in flight 35.5-35.9 -> 37.2-37.3/s; zelana_batch 81.3-81.6
+// -> 84.8-85.0/s).  0: the round-5 order (all MSMs, then the witness map).
+#ifndef ZK_G2_AFTER_WM
+#define ZK_G2_AFTER_WM 1
+#endif
   if (n <= SMALL_PROOF_MAX) {
     rc = prove_submit_small(ctx, pk, dr, dz, logn, dh, jobs);
+  } else if (ZK_G2_AFTER_WM && pk->d_bidx) {
+    // The witness map's NTTs are the path to the h MSM.  Beside the G2
+    // accumulation (248 VGPRs, 2 waves per SIMD) no NTT wave fits on a SIMD;
+    // beside the G1 ones (3 waves, LDS-capped) one does.  So the witness map is
+    // queued first, the z-weighted MSMs fork from before it, and the G2
+    // accumulation (b_g2, sharing b_g1's sort) waits for its end; the h MSM
+    // then runs beside the G2 accumulation.
+    if (!ctx->prove_fork) ZK_HIP(hipEventCreateWithFlags(&ctx->prove_fork, hipEventDisableTiming));
+    if (!ctx->wm_done) ZK_HIP(hipEventCreateWithFlags(&ctx->wm_done, hipEventDisableTiming));
+    uint32_t* zb;
+    rc = ctx->ws.get("g16_zb", pk->nb_c * 32, (void**)&zb);
+    if (!rc) {
+      k_gather_scalars<<<(unsigned)((pk->nb_c + 255) / 256), 256, 0, ctx->stream>>>(dz, pk->d_bidx, pk->nb_c, zb);
+      rc = hipGetLastError() == hipSuccess ? 0 : ZKMI_EHIP;
+    }
+    if (!rc) rc = hipEventRecord(ctx->prove_fork, ctx->stream) == hipSuccess ? 0 : ZKMI_EHIP;
+    if (!rc) rc = witness_map_dev(ctx, dr, dz, logn, dh);
+    if (!rc) rc = hipEventRecord(ctx->wm_done, ctx->stream) == hipSuccess ? 0 : ZKMI_EHIP;
+    ctx->msm_fork = ctx->prove_fork;
+    if (!rc) rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
+    if (!rc) rc = msm_submit(ctx, pk->a_query, 1, dz + 8, nv - 1, &jobs[2]);
+    ctx->acc_gate = ctx->wm_done;
+    ctx->acc_gate_set = pk->b_g2_c;
+    const zkmi_bases* bq[2] = {pk->b_g1_c, pk->b_g2_c};
+    if (!rc) rc = msm_submit_shared(ctx, bq, 2, 0, zb, pk->nb_c, &jobs[3]);
+    ctx->acc_gate = nullptr;
+    ctx->acc_gate_set = nullptr;
+    ctx->msm_fork = nullptr;  // h forks after the witness map
+    if (!rc) rc = msm_submit(ctx, pk->h_query_rev, 0, dh, n - 1, &jobs[0]);
   } else {
   rc = msm_submit(ctx, pk->l_query, 0, dz + l * 8, w, &jobs[1]);
   if (!rc && pk->d_bidx) {  // a over z[1..V]; b1 / b2 over the compacted B variables

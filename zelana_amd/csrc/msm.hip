@@ -3251,6 +3251,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
 
 static int msm_acc_any(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const zkmi_bases* tb, size_t offset, size_t n,
                        const uint32_t* sval, const uint32_t* bstart, zkmi_msm_job* job) {
+  if (ctx->acc_gate && tb == ctx->acc_gate_set) ZK_HIP(hipStreamWaitEvent(lane->st, ctx->acc_gate, 0));
   return tb->g2 ? msm_acc_phase<G2T>(ctx, lane, P, tb, offset, n, sval, bstart, job)
                 : msm_acc_phase<G1T>(ctx, lane, P, tb, offset, n, sval, bstart, job);
 }

@@ -196,6 +196,7 @@ void zkmi_ctx_destroy(zkmi_ctx* ctx) {
   ctx->lanes.clear();
   ctx->nstreams = 1;
   if (ctx->prove_fork) hipEventDestroy(ctx->prove_fork);
+  if (ctx->wm_done) hipEventDestroy(ctx->wm_done);
   for (auto& pb : ctx->pinned_free) hipHostFree(pb.first);
   ctx->pinned_free.clear();
   ctx->pinned_size.clear();

@@ -87,6 +87,11 @@ struct zkmi_ctx {
   // lane) starts after it (msm.hip msm_acc_phase)
   zk::MsmLane* acc_last = nullptr;
   hipEvent_t prove_fork = nullptr;  // owned: the event groth16_prove_submit uses for it
+  // set: the accumulation of base set acc_gate_set waits on this event
+  // (groth16 large proofs: the G2 accumulation after the witness map)
+  hipEvent_t acc_gate = nullptr;
+  const zkmi_bases* acc_gate_set = nullptr;
+  hipEvent_t wm_done = nullptr;  // owned: end of a large proof's witness map
   // Stream budget: communicators alive on this context, and the
   // streams the library holds for it (context, lanes, communicators', witness
   // programs').  While a communicator exists the lanes are capped at
