@@ -49,11 +49,35 @@ __device__ Fe fe_pow_u64(Fe base, uint64_t e) {
 // Twiddle table omega^e, e < half, reduced, stored UNPACKED (9 x 29-bit limbs)
 // in two planes so the butterflies skip the 8 -> 9 limb unpack: limbs 0..7
 // at tw[8e..8e+8) (two 16-B loads), limb 8 at tw[8 half + e].
-__device__ __forceinline__ Fe ld_tw(const uint32_t* __restrict__ tw, uint64_t half, uint64_t e) {
-  const uint4* p = reinterpret_cast<const uint4*>(tw + e * 8);
+//
+// ZK_NTT_STAGE_TW: the table is stage-major instead: 2 half slots, slot
+// h + i (h a power of two <= half, i < h) = omega_{2h}^i, the twiddle of pair
+// i of a stage with pair distance h; limbs 0..7 at tw[8 slot], limb 8 at
+// tw[16 half + slot].  Slots [half, 2 half) are the plain table.  A stage
+// with distance h then reads h contiguous slots instead of every (half/h)-th
+// entry of the plain table, whose 36-B entries at strides >= 64 B pulled a
+// whole line per twiddle: ~1.1 GB of twiddle fetch in the first pass of a
+// 2^24 transform against ~0.6 GB stage-major.  Measured (round 6, one box,
+// 3 interleaved repeats, tools/r06_ntt_ab.sh): 2^24 NTT+INTT 3.91-3.97 ->
+// 3.74 ms, 2^22 1.00 -> 0.97-0.98 ms.  Twice the table memory (n x 36 B).
+#ifndef ZK_NTT_STAGE_TW
+#define ZK_NTT_STAGE_TW 1
+#endif
+__device__ __forceinline__ Fe ld_tw_slot(const uint32_t* __restrict__ tw, uint64_t l8, uint64_t slot) {
+  const uint4* p = reinterpret_cast<const uint4*>(tw + slot * 8);
   const uint4 a = p[0], b = p[1];
-  return Fe{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, tw[8 * half + e]}};
+  return Fe{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, tw[l8 + slot]}};
 }
+__device__ __forceinline__ Fe ld_tw(const uint32_t* __restrict__ tw, uint64_t half, uint64_t e) {
+  if (ZK_NTT_STAGE_TW) return ld_tw_slot(tw, 16 * half, half + e);
+  return ld_tw_slot(tw, 8 * half, e);
+}
+// twiddle of pair i < h of a stage with pair distance h (= omega_n^(i half / h))
+__device__ __forceinline__ Fe ld_tw_stage(const uint32_t* __restrict__ tw, uint64_t half, uint64_t h, uint64_t i) {
+  if (ZK_NTT_STAGE_TW) return ld_tw_slot(tw, 16 * half, h + i);
+  return ld_tw_slot(tw, 8 * half, i * (half / h));
+}
+static constexpr uint64_t ntt_tw_words(uint64_t half) { return (ZK_NTT_STAGE_TW ? 2 : 1) * half * 9; }
 // Each thread: one pow + 63 muls for a run of 64.
 __global__ void __launch_bounds__(256) k_ntt_twiddles(uint32_t* __restrict__ tw, uint32_t logn, int inv, uint64_t half) {
   uint64_t run = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -61,13 +85,23 @@ __global__ void __launch_bounds__(256) k_ntt_twiddles(uint32_t* __restrict__ tw,
   if (e0 >= half) return;
   Fe w = root_of_unity(logn, inv != 0);
   Fe cur = fe_pow_u64(w, e0);
+  const uint64_t s0 = ZK_NTT_STAGE_TW ? half : 0, l8 = ZK_NTT_STAGE_TW ? 16 * half : 8 * half;
   for (int k = 0; k < 64 && e0 + k < half; k++) {
     const Fe v = reduce<FrP>(cur);
 #pragma unroll
-    for (int l = 0; l < 8; l++) tw[(e0 + k) * 8 + l] = v.v[l];
-    tw[8 * half + e0 + k] = v.v[8];
+    for (int l = 0; l < 8; l++) tw[(s0 + e0 + k) * 8 + l] = v.v[l];
+    tw[l8 + s0 + e0 + k] = v.v[8];
     cur = mul<FrP>(cur, w);
   }
+}
+// stage-major slots [1, half) from the plain slots [half, 2 half)
+__global__ void __launch_bounds__(256) k_ntt_tw_levels(uint32_t* __restrict__ tw, uint64_t half) {
+  const uint64_t slot = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (slot == 0 || slot >= half) return;
+  const uint64_t h = 1ull << (63 - __clzll((long long)slot)), e = (slot - h) * (half / h);
+#pragma unroll
+  for (int l = 0; l < 8; l++) tw[slot * 8 + l] = tw[(half + e) * 8 + l];
+  tw[16 * half + slot] = tw[16 * half + half + e];
 }
 
 // One group of `k` <= 8 stages over a tile of 2048 elements.  Sub-transform
@@ -174,7 +208,7 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint3
       const uint32_t col = (g.q0 + ((e0 & g.smask) << g.qsh)) & g.colmask;
       const uint32_t jj = (e0 >> g.lsub) & ((1u << lhl) - 1);
       // omega_m^(i mod m/2) = omega_n^((i mod m/2) * n/m)
-      w[p] = ld_tw(tw, half, (uint64_t)((col + (jj << g.colbits)) << sh));
+      w[p] = ld_tw_stage(tw, half, half >> sh, (uint64_t)(col + (jj << g.colbits)));
     }
 #pragma unroll
     for (int p = 0; p < NP; p++) {
@@ -511,10 +545,11 @@ static int get_twiddles(zkmi_ctx* ctx, uint32_t logn, int inv, const uint32_t** 
   bool fresh = ctx->ws.bufs.find(name) == ctx->ws.bufs.end();
   uint64_t half = std::max<uint64_t>(1, (1ull << logn) / 2);
   uint32_t* tw;
-  ZK_TRY(ctx->ws.get(name, half * 36, (void**)&tw));
+  ZK_TRY(ctx->ws.get(name, ntt_tw_words(half) * 4, (void**)&tw));
   if (fresh) {
     uint64_t runs = (half + 63) / 64;
     k_ntt_twiddles<<<(unsigned)((runs + 255) / 256), 256, 0, ctx->stream>>>(tw, logn, inv, half);
+    if (ZK_NTT_STAGE_TW && half > 1) k_ntt_tw_levels<<<(unsigned)((half + 255) / 256), 256, 0, ctx->stream>>>(tw, half);
     ZK_HIP(hipGetLastError());
   }
   *out = tw;
