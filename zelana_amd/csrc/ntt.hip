@@ -68,18 +68,46 @@ __device__ __forceinline__ Fe ld_tw_slot(const uint32_t* __restrict__ tw, uint64
   const uint4 a = p[0], b = p[1];
   return Fe{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, tw[l8 + slot]}};
 }
+// (small transforms only: log n < 11, no limb-8 permutation)
 __device__ __forceinline__ Fe ld_tw(const uint32_t* __restrict__ tw, uint64_t half, uint64_t e) {
   if (ZK_NTT_STAGE_TW) return ld_tw_slot(tw, 16 * half, half + e);
   return ld_tw_slot(tw, 8 * half, e);
 }
-// twiddle of pair i < h of a stage with pair distance h (= omega_n^(i half / h))
-__device__ __forceinline__ Fe ld_tw_stage(const uint32_t* __restrict__ tw, uint64_t half, uint64_t h, uint64_t i) {
-  if (ZK_NTT_STAGE_TW) return ld_tw_slot(tw, 16 * half, h + i);
-  return ld_tw_slot(tw, 8 * half, i * (half / h));
-}
 static constexpr uint64_t ntt_tw_words(uint64_t half) { return (ZK_NTT_STAGE_TW ? 2 : 1) * half * 9; }
+// ZK_NTT_TW_L8P: limb 8 of the outermost group's stages (pair distance h >=
+// 2^cb0, cb0 = log n - k0, k0 = that group's stage count) is stored
+// workgroup-major.  Such a stage's pair i = col + jj 2^cb0 (col < 2^cb0) is
+// read by the workgroup of columns col >> L (L = 10 - k0, 2^L adjacent
+// columns per 1024-element tile); its limb-8 word goes to slot position
+// h + (((col >> L) (h >> cb0) + jj) << L) + (col mod 2^L), so one workgroup's
+// limb-8 words of a stage are contiguous (2 KB) instead of 16 B per 128-B
+// line.  Limbs 0..7 are 4 adjacent slots = one full line either way.
+// Measured (round 6, one box, 3 interleaved repeats): first-pass fetch at
+// 2^24 1.61 -> 1.14 GB (PMC, FETCH_SIZE x 2), 2^24 NTT+INTT 3.80-3.81 ->
+// 3.79-3.80 ms, 2^22 0.978-0.987 -> 0.971-0.975 ms: the pass is issue-bound
+// (0.84-0.86), so the bytes saved show little in its time.
+#ifndef ZK_NTT_TW_L8P
+#define ZK_NTT_TW_L8P 1
+#endif
+__host__ __device__ __forceinline__ uint64_t ntt_l8_pos(uint64_t h, uint64_t i, uint32_t cb0, uint32_t L) {
+  if (!ZK_NTT_TW_L8P || !ZK_NTT_STAGE_TW || cb0 == 0 || h < (1ull << cb0)) return h + i;
+  const uint64_t col = i & ((1ull << cb0) - 1), jj = i >> cb0;
+  return h + ((((col >> L) * (h >> cb0)) + jj) << L) + (col & ((1ull << L) - 1));
+}
+// twiddle of pair i < h of a stage with pair distance h (= omega_n^(i half / h));
+// l8: the slot of its limb 8 (ntt_l8_pos; h + i outside the outermost group)
+__device__ __forceinline__ Fe ld_tw_stage(const uint32_t* __restrict__ tw, uint32_t half, uint32_t h, uint32_t i,
+                                          uint32_t l8) {
+  if (ZK_NTT_STAGE_TW) {
+    const uint4* p = reinterpret_cast<const uint4*>(tw + (size_t)(h + i) * 8);
+    const uint4 a = p[0], b = p[1];
+    return Fe{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, tw[(size_t)16 * half + l8]}};
+  }
+  return ld_tw_slot(tw, 8 * (uint64_t)half, (uint64_t)i * (half / h));
+}
 // Each thread: one pow + 63 muls for a run of 64.
-__global__ void __launch_bounds__(256) k_ntt_twiddles(uint32_t* __restrict__ tw, uint32_t logn, int inv, uint64_t half) {
+__global__ void __launch_bounds__(256) k_ntt_twiddles(uint32_t* __restrict__ tw, uint32_t logn, int inv, uint64_t half,
+                                                      uint32_t cb0, uint32_t L) {
   uint64_t run = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   uint64_t e0 = run * 64;
   if (e0 >= half) return;
@@ -90,18 +118,19 @@ __global__ void __launch_bounds__(256) k_ntt_twiddles(uint32_t* __restrict__ tw,
     const Fe v = reduce<FrP>(cur);
 #pragma unroll
     for (int l = 0; l < 8; l++) tw[(s0 + e0 + k) * 8 + l] = v.v[l];
-    tw[l8 + s0 + e0 + k] = v.v[8];
+    tw[l8 + (ZK_NTT_STAGE_TW ? ntt_l8_pos(half, e0 + k, cb0, L) : e0 + k)] = v.v[8];
     cur = mul<FrP>(cur, w);
   }
 }
 // stage-major slots [1, half) from the plain slots [half, 2 half)
-__global__ void __launch_bounds__(256) k_ntt_tw_levels(uint32_t* __restrict__ tw, uint64_t half) {
+__global__ void __launch_bounds__(256) k_ntt_tw_levels(uint32_t* __restrict__ tw, uint64_t half, uint32_t cb0,
+                                                       uint32_t L) {
   const uint64_t slot = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (slot == 0 || slot >= half) return;
   const uint64_t h = 1ull << (63 - __clzll((long long)slot)), e = (slot - h) * (half / h);
 #pragma unroll
   for (int l = 0; l < 8; l++) tw[slot * 8 + l] = tw[(half + e) * 8 + l];
-  tw[16 * half + slot] = tw[16 * half + half + e];
+  tw[16 * half + ntt_l8_pos(h, slot - h, cb0, L)] = tw[16 * half + ntt_l8_pos(half, e, cb0, L)];
 }
 
 // One group of `k` <= 8 stages over a tile of 2048 elements.  Sub-transform
@@ -208,7 +237,12 @@ __device__ __forceinline__ void ntt_r8_stages(Fe (&x)[EPT], uint32_t base, uint3
       const uint32_t col = (g.q0 + ((e0 & g.smask) << g.qsh)) & g.colmask;
       const uint32_t jj = (e0 >> g.lsub) & ((1u << lhl) - 1);
       // omega_m^(i mod m/2) = omega_n^((i mod m/2) * n/m)
-      w[p] = ld_tw_stage(tw, half, half >> sh, (uint64_t)(col + (jj << g.colbits)));
+      const uint32_t h = (uint32_t)(half >> sh), i = col + (jj << g.colbits);
+      // outermost group (ntt_l8_pos): pair i = col + jj 2^colbits, h = 2^(colbits + lhl)
+      const uint32_t l8 = (ZK_NTT_TW_L8P && g.a == g.logn)
+                              ? h + (((((col >> g.lsub) << lhl) | jj) << g.lsub) | (col & g.smask))
+                              : h + i;
+      w[p] = ld_tw_stage(tw, (uint32_t)half, h, i, l8);
     }
 #pragma unroll
     for (int p = 0; p < NP; p++) {
@@ -548,8 +582,12 @@ static int get_twiddles(zkmi_ctx* ctx, uint32_t logn, int inv, const uint32_t** 
   ZK_TRY(ctx->ws.get(name, ntt_tw_words(half) * 4, (void**)&tw));
   if (fresh) {
     uint64_t runs = (half + 63) / 64;
-    k_ntt_twiddles<<<(unsigned)((runs + 255) / 256), 256, 0, ctx->stream>>>(tw, logn, inv, half);
-    if (ZK_NTT_STAGE_TW && half > 1) k_ntt_tw_levels<<<(unsigned)((half + 255) / 256), 256, 0, ctx->stream>>>(tw, half);
+    // the outermost group of the 1024-element tile plan (ntt_groups)
+    const uint32_t k0 = logn >= 11 ? (logn + ((logn + 7) / 8) - 1) / ((logn + 7) / 8) : 0;
+    const uint32_t cb0 = logn >= 11 ? logn - k0 : 0, L = logn >= 11 ? 10 - k0 : 0;
+    k_ntt_twiddles<<<(unsigned)((runs + 255) / 256), 256, 0, ctx->stream>>>(tw, logn, inv, half, cb0, L);
+    if (ZK_NTT_STAGE_TW && half > 1)
+      k_ntt_tw_levels<<<(unsigned)((half + 255) / 256), 256, 0, ctx->stream>>>(tw, half, cb0, L);
     ZK_HIP(hipGetLastError());
   }
   *out = tw;
@@ -585,6 +623,7 @@ static std::vector<uint32_t> ntt_groups(uint32_t logn) {
 #ifndef ZK_NTT_TB_OUTER
 #define ZK_NTT_TB_OUTER 10
 #endif
+static_assert(!ZK_NTT_TW_L8P || ZK_NTT_TB_OUTER == 10, "the limb-8 layout assumes 1024-element outer tiles");
 template <bool DIT, int PRO, int EPI, bool PERM>
 static void launch_group(hipStream_t st, const uint32_t* src, uint32_t* dst, const uint32_t* tw, uint32_t logn,
                          uint32_t a, uint32_t k, const NttIo& io) {
