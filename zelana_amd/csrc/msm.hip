@@ -1421,6 +1421,25 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
 // pass).  The rare
 // states (a base at infinity, the empty or one-point accumulator after a
 // cancellation) branch per lane; lanes of a wave have equal trip counts.
+// ZK_ACC_NT: table-row gathers of the one-lane-per-bucket G1 accumulation as
+// non-temporal loads (every row is read once per MSM)
+#ifndef ZK_ACC_NT
+#define ZK_ACC_NT 0
+#endif
+__device__ __forceinline__ void ld_row4(uint4 (&r)[4], const uint4* q) {
+  if constexpr (ZK_ACC_NT) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* qq = reinterpret_cast<const u32x4*>(q);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const u32x4 t = __builtin_nontemporal_load(qq + k);
+      r[k] = make_uint4(t.x, t.y, t.z, t.w);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) r[k] = q[k];
+  }
+}
 __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, const uint32_t* __restrict__ nover,
                                               uint32_t nmain, const uint32_t* __restrict__ sval,
                                               const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
@@ -1474,22 +1493,14 @@ __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, c
   uint4 raw[4];
   const uint32_t last = end - 1;
   uint32_t v_nxt = sval[start];
-  {
-    const uint4* q = row(v_nxt);
-#pragma unroll
-    for (int k = 0; k < 4; k++) raw[k] = q[k];
-  }
+  ld_row4(raw, row(v_nxt));
   uint32_t v_nn = sval[min(start + 1, last)];
   for (uint32_t p = start; p < end; p++) {
     uint4 cr[4];
     const uint32_t v = v_nxt;
 #pragma unroll
     for (int k = 0; k < 4; k++) cr[k] = raw[k];
-    {
-      const uint4* q = row(v_nn);
-#pragma unroll
-      for (int k = 0; k < 4; k++) raw[k] = q[k];
-    }
+    ld_row4(raw, row(v_nn));
     v_nxt = v_nn;
     v_nn = sval[min(p + 2, last)];
     step(cr, v);
