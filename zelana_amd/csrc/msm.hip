@@ -322,9 +322,9 @@ __device__ __forceinline__ uint32_t rs_block_scan(const uint32_t* hist, uint32_t
 // written lines get evicted (measured: ~10x slower than the reads).
 // LDS layout: hist[nb] | lstart[nb] | gbase[nb] | tmp[4] | skey[RS_ST] | sval[RS_ST]
 // Four barriers per sub-tile; hist is zeroed by the caller's first barrier.
-template <int PER, class Fill, class Bin, bool WRITE_KEY, int T = RS_THREADS>
+template <int PER, class Fill, class Bin, bool WRITE_KEY, int T = RS_THREADS, class KT = uint32_t>
 __device__ __forceinline__ void rs_scatter_core(uint32_t nsub, uint32_t nb, uint32_t* lds, Fill fill, Bin bin,
-                                                 uint32_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+                                                 KT* __restrict__ okey, uint32_t* __restrict__ oval) {
   uint32_t* hist = lds;
   uint32_t* lstart = lds + nb;
   uint32_t* gbase = lds + 2 * nb;
@@ -355,7 +355,7 @@ __device__ __forceinline__ void rs_scatter_core(uint32_t nsub, uint32_t nb, uint
     for (uint32_t q = threadIdx.x; q < total; q += T) {
       uint32_t kk = skey[q], bn = bin(kk);
       uint32_t g = gbase[bn] + (q - lstart[bn]);
-      if (WRITE_KEY) okey[g] = kk;
+      if (WRITE_KEY) okey[g] = (KT)kk;
       oval[g] = sval[q];
     }
     __syncthreads();
@@ -663,6 +663,15 @@ __global__ void __launch_bounds__(256) k_rs_bstart(const uint32_t* __restrict__ 
 // of a 3.9M-entry [bin][lo][tile] count matrix alone sat ~150 us on the
 // critical path between two accumulations.)
 constexpr uint32_t BS_NSC = 32;  // super-chunks
+// ZK_BS_KEY16: the first scatter writes only the low 16 bits of each key (the
+// bin is implied by the position; the second pass needs the low lob <= 11
+// bits), so okey is read and written at 2 B per entry instead of 4
+// (measured, round 6: 2^26 MSM 63.24-63.30 -> 62.67-62.70 ms, 2^20 2-lane
+// loop 916.7-917.9 -> 917.6-920.7 Mpt/s, one box)
+#ifndef ZK_BS_KEY16
+#define ZK_BS_KEY16 1
+#endif
+using BsKey = std::conditional_t<ZK_BS_KEY16 != 0, uint16_t, uint32_t>;
 
 // exclusive prefix, in index order, of get(0..nb) into out[0..nb) (LDS) by T
 // threads; returns the total.  tmp: T/64 words of LDS.  Ends with a barrier.
@@ -737,7 +746,7 @@ __global__ void __launch_bounds__(T) k_bs_scatter1(const uint32_t* __restrict__ 
                                                    uint32_t wsel, uint32_t NH, uint32_t lob, uint32_t CS, uint32_t scs,
                                                    const uint32_t* __restrict__ bintot,
                                                    const uint32_t* __restrict__ sctot,
-                                                   const uint32_t* __restrict__ choff, uint32_t* __restrict__ okey,
+                                                   const uint32_t* __restrict__ choff, BsKey* __restrict__ okey,
                                                    uint32_t* __restrict__ oval) {
   ZK_TAIL_WAVE();
   extern __shared__ uint32_t lds[];
@@ -781,7 +790,7 @@ __device__ __forceinline__ uint32_t bs_tiles(const uint32_t* __restrict__ bintot
   return TT;
 }
 
-__global__ void __launch_bounds__(256) k_bs_count2(const uint32_t* __restrict__ okey,
+__global__ void __launch_bounds__(256) k_bs_count2(const BsKey* __restrict__ okey,
                                                    const uint32_t* __restrict__ bintot, uint32_t NH, uint32_t lob,
                                                    uint32_t C2, uint32_t T2max, uint32_t* __restrict__ thist) {
   ZK_TAIL_WAVE();
@@ -842,7 +851,7 @@ struct ItemsOut {
 };
 
 template <int ST, bool ITEMS>
-__global__ void __launch_bounds__(256) k_bs_scatter2(const uint32_t* __restrict__ okey,
+__global__ void __launch_bounds__(256) k_bs_scatter2(const BsKey* __restrict__ okey,
                                                      const uint32_t* __restrict__ oval,
                                                      const uint32_t* __restrict__ bintot, uint32_t NH, uint32_t lob,
                                                      uint32_t C2, uint32_t T2max, uint32_t K,
@@ -1421,24 +1430,11 @@ __device__ __forceinline__ void acc_items_body(const uint4* __restrict__ items, 
 // pass).  The rare
 // states (a base at infinity, the empty or one-point accumulator after a
 // cancellation) branch per lane; lanes of a wave have equal trip counts.
-// ZK_ACC_NT: table-row gathers of the one-lane-per-bucket G1 accumulation as
-// non-temporal loads (every row is read once per MSM)
-#ifndef ZK_ACC_NT
-#define ZK_ACC_NT 0
-#endif
 __device__ __forceinline__ void ld_row4(uint4 (&r)[4], const uint4* q) {
-  if constexpr (ZK_ACC_NT) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4* qq = reinterpret_cast<const u32x4*>(q);
+  // (Tried, round 6: non-temporal loads here -- every row is read once per
+  // MSM -- 2^20 2-lane loop 917 -> 875 Mpt/s, 2^26 63.3 -> 65.3 ms.)
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const u32x4 t = __builtin_nontemporal_load(qq + k);
-      r[k] = make_uint4(t.x, t.y, t.z, t.w);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; k++) r[k] = q[k];
-  }
+  for (int k = 0; k < 4; k++) r[k] = q[k];
 }
 __device__ __forceinline__ void acc_items_g1f(const uint4* __restrict__ items, const uint32_t* __restrict__ nover,
                                               uint32_t nmain, const uint32_t* __restrict__ sval,
@@ -2772,7 +2768,7 @@ static void launch_bs_p1(hipStream_t st, const uint32_t* sc, size_t n, int Wp, u
   uint32_t* sctot = ctr + g.NH + 16;
   if (scatter)
     k_bs_scatter1<C, 256, BAL><<<g.nf, 256, rs_scatter_lds(g.NH, 256 * W, 256), st>>>(
-        sc, n, Wp, B, wsel, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff, okey, oval);
+        sc, n, Wp, B, wsel, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff, reinterpret_cast<BsKey*>(okey), oval);
   else
     k_bs_count<C, BAL><<<g.nf, 256, g.NH * 4, st>>>(sc, n, Wp, B, wsel, g.NH, g.lob, g.CS, g.scs, bintot, sctot, choff,
                                                     next_ctr, (uint32_t)g.ctr_words());
@@ -2899,14 +2895,14 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
     ZK_HIP(hipEventRecord(lane->consumed, st));
     ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
     const uint32_t gt = ((g.T2max + 7) / 8) * 8;  // XCD-mapped grid (rs_xcd_tile)
-    k_bs_count2<<<gt, 256, (g.NLO + 2 * g.NH + 2 + 4) * 4, st>>>(okey, ctr, g.NH, g.lob, g.C2, g.T2max, thist);
+    k_bs_count2<<<gt, 256, (g.NLO + 2 * g.NH + 2 + 4) * 4, st>>>(reinterpret_cast<BsKey*>(okey), ctr, g.NH, g.lob, g.C2, g.T2max, thist);
     if (items) {
-      k_bs_scatter2<BS_ST, true><<<gt, 256, bs_lds_scatter2(g), st>>>(okey, oval, ctr, g.NH, g.lob, g.C2, g.T2max,
+      k_bs_scatter2<BS_ST, true><<<gt, 256, bs_lds_scatter2(g), st>>>(reinterpret_cast<BsKey*>(okey), oval, ctr, g.NH, g.lob, g.C2, g.T2max,
                                                                      P.K, thist, sval, bstart, io);
       k_items_place<<<g.NH, 256, 0, st>>>(stage, g.NLO, io.cap, io.ghist, io.ghist + ITEM_CAP_MAX + 1, it,
                                           (uint32_t)g.nmain);
     } else {
-      k_bs_scatter2<BS_ST, false><<<gt, 256, bs_lds_scatter2(g), st>>>(okey, oval, ctr, g.NH, g.lob, g.C2, g.T2max,
+      k_bs_scatter2<BS_ST, false><<<gt, 256, bs_lds_scatter2(g), st>>>(reinterpret_cast<BsKey*>(okey), oval, ctr, g.NH, g.lob, g.C2, g.T2max,
                                                                       P.K, thist, sval, bstart, io);
     }
     lane->bs_cur = ctr;  // the accumulation phases of this sort read its item counters
