@@ -120,7 +120,9 @@ def test_msm_rejects_off_curve(ctx):
         ctx.bases_g1(pts)
 
 
-@pytest.mark.parametrize("log_n", [1, 2, 5, 10, 11, 13, 16])
+# 11..19 cover every group plan shape of the stage-major twiddle table (2 and
+# 3 passes, outer tiles of 2^(10 - k0) columns with k0 = 6, 7, 8)
+@pytest.mark.parametrize("log_n", [1, 2, 5, 10, 11, 12, 13, 16, 17, 19])
 @pytest.mark.parametrize("inverse,coset", [(False, False), (True, False), (False, True), (True, True)])
 def test_ntt_vs_oracle(ctx, log_n, inverse, coset):
     data = O.gen_scalars(log_n * 11 + inverse * 2 + coset, 1 << log_n)
