@@ -5,6 +5,11 @@
 set -o pipefail
 OUT=gpurun_out/${TAG:-r06ab2}
 mkdir -p $OUT
+for v in ${VTEST:-}; do
+  ZKMI_LIB=zelana_amd/_ab/libzkmi_$v.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+    -m gpu ${TESTS:-tests/test_gpu_groth16.py} > $OUT/tests_$v.log 2>&1 || { tail -n 20 $OUT/tests_$v.log; exit 1; }
+  tail -n 1 $OUT/tests_$v.log
+done
 for rep in 1 2; do
   for v in ${VARIANTS:-base}; do
     echo "== $v rep $rep" >> $OUT/ab.log
@@ -17,10 +22,10 @@ for rep in 1 2; do
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 e = d["extra"]
-z, c = e["zelana_batch_proofs"], e["config1_l2_small"]
+z, c = e["zelana_batch_proofs"], e.get("config1_l2_small", {})
 print(json.dumps({"v": sys.argv[2], "zb": z["proofs_per_s"], "zb_two": z["two_in_flight"]["proofs_per_s"],
-                  "zb_e2e4": z["end_to_end"]["batched"]["proofs_per_s"], "c1_res": c["gpu_prove_resident_ms"],
-                  "c1_nat": c["native_prove_ms"]}))
+                  "zb_e2e4": z["end_to_end"]["batched"]["proofs_per_s"], "c1_res": c.get("gpu_prove_resident_ms"),
+                  "c1_nat": c.get("native_prove_ms")}))
 PY
     fi
   done
