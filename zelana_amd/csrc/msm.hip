@@ -1114,7 +1114,9 @@ __global__ void __launch_bounds__(256) k_msm_cutsum_coop(const uint32_t* __restr
                                                          uint32_t* __restrict__ buckets,
                                                          uint32_t* __restrict__ xvalid,
                                                          const uint32_t* __restrict__ xpts,
-                                                         uint32_t* __restrict__ open_flag) {
+                                                         uint32_t* __restrict__ open_flag,
+                                                         uint4* __restrict__ split = nullptr,
+                                                         uint32_t* __restrict__ nsplit = nullptr) {
   ZK_TAIL_WAVE();
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
@@ -1132,8 +1134,11 @@ __global__ void __launch_bounds__(256) k_msm_cutsum_coop(const uint32_t* __restr
       live = k > 1;  // else complete inside one chunk: already in buckets[b]
     }
   }
-  if (live && k > 16) {  // left to the k_msm_accN cascade
-    if (r == 0) atomicOr(open_flag, 1u);
+  if (live && k > 16) {  // left to the k_msm_accN cascade, or listed for k_split_combine<G, true>
+    if (r == 0) {
+      atomicOr(open_flag, 1u);
+      if (split) split[atomicAdd(nsplit, 1u)] = make_uint4(b, t0, k, 0);
+    }
     live = false;
   }
   bool has = live && r < k;
@@ -1576,7 +1581,10 @@ __global__ void __launch_bounds__(256) k_items_place(const uint4* __restrict__ s
 // One curve-addition call site in one block-uniform step loop (a second
 // inlined copy spills G2).  A uniform MSM splits nothing: the launch reads
 // the count and exits.
-template <class G>
+// CHUNKED: the pieces are a chunked accumulation's partials (k_msm_acc0) of a
+// bucket cut by chunk edges t0..t0 + np - 1 (split entry: key, t0, np): piece
+// 0 is chunk t0's tail slot, piece r >= 1 chunk t0 + r's head slot.
+template <class G, bool CHUNKED = false>
 __global__ void __launch_bounds__(256) k_split_combine(const uint4* __restrict__ split,
                                                        const uint32_t* __restrict__ nsplit,
                                                        const uint32_t* __restrict__ xpts,
@@ -1634,7 +1642,8 @@ __global__ void __launch_bounds__(256) k_split_combine(const uint4* __restrict__
       if (k < nload) {
         const uint32_t pc = (stride == 64 ? lane : threadIdx.x) + stride * k;
         if (mine_in && pc < cur.z) {
-          q = ld_xyzz<G>(xpts + (size_t)(cur.y + pc) * XW);
+          const uint32_t slot = CHUNKED ? (pc == 0 ? 2 * cur.y + 2 : 2 * (cur.y + pc) + 1) : cur.y + pc;
+          q = ld_xyzz<G>(xpts + (size_t)slot * XW);
           act = !xyzz_is_inf(q);
         }
       } else if (k < nload + lev) {  // in-wave tree
@@ -3188,6 +3197,25 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       ZK_HIP(hipGetLastError());
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);
+    // Small MSMs (ZK_SMALL_SPLIT): the buckets cut by more than 16 chunk edges
+    // (a witness MSM's small digits) are listed by the cut sums and summed by
+    // k_split_combine in one launch -- a block-wide tree per bucket -- instead
+    // of the k_msm_accN cascade's ~7 launches, most of which exit at once.
+    // Measured (round 6, one box, 3 interleaved repeats of tools/small_prove.py):
+    // configs[0] resident prove 1.754-1.768 -> 1.536-1.579 ms, same proof bytes.
+#ifndef ZK_SMALL_SPLIT
+#define ZK_SMALL_SPLIT 1
+#endif
+    if (ZK_SMALL_SPLIT && K <= CUTSUM_COOP_K) {
+      const size_t maxsplit = std::min<size_t>(K, nch / 16 + 1);
+      uint4* split;
+      ZK_TRY(ws.get("msm_small_split", maxsplit * 16, (void**)&split));
+      k_msm_cutsum_coop<GS><<<(unsigned)(((size_t)K * 16 + 255) / 256), 256, 0, st>>>(bstart, K, L, buckets, xvalid,
+                                                                                   xpts, &flags[0], split, &flags[32]);
+      k_split_combine<GS, true><<<(unsigned)std::min<size_t>((maxsplit + 3) / 4, 256), 256, 0, st>>>(split, &flags[32],
+                                                                                                  xpts, buckets);
+      ZK_HIP(hipGetLastError());
+    } else {
     if (K <= CUTSUM_COOP_K)
       k_msm_cutsum_coop<GS><<<(unsigned)(((size_t)K * 16 + 255) / 256), 256, 0, st>>>(bstart, K, L, buckets, xvalid,
                                                                                    xpts, &flags[0]);
@@ -3218,6 +3246,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
       cur_len = nc == 1 ? 1 : 2 * nc + 1;
     }
     ZK_HIP(hipGetLastError());
+    }
   }
   // bucket reduction -> W*(bb+1) canonical bit sums.  (Tried: the reduction
   // and hand-over on a second stream with double-buffered buckets, so the
