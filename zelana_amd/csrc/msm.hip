@@ -456,7 +456,7 @@ __global__ void __launch_bounds__(256) k_ss_count(const uint32_t* __restrict__ s
 }
 // one 1024-thread workgroup: bstart[k] = sum of cnt[< k], bstart[K] = total,
 // cursor = a copy of bstart[0..K)
-__global__ void __launch_bounds__(1024) k_ss_scan(const uint32_t* __restrict__ cnt, uint32_t K,
+__global__ void __launch_bounds__(1024) k_ss_scan(uint32_t* __restrict__ cnt, uint32_t K,
                                                   uint32_t* __restrict__ bstart, uint32_t* __restrict__ cursor) {
   ZK_TAIL_WAVE();
   __shared__ uint32_t wsum[16];
@@ -483,6 +483,7 @@ __global__ void __launch_bounds__(1024) k_ss_scan(const uint32_t* __restrict__ c
     bstart[k] = run;
     cursor[k] = run;
     run += cnt[k];
+    cnt[k] = 0;  // clean for the lane's next counting sort (no memset launch)
   }
   if (threadIdx.x == 0) bstart[K] = total;
 }
@@ -1171,10 +1172,13 @@ __device__ __forceinline__ void msm_acc0_body(const uint32_t* __restrict__ sval,
                                                   const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
                                                   uint32_t* __restrict__ buckets,
                                                   uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                                                  uint32_t* __restrict__ xpts) {
+                                                  uint32_t* __restrict__ xpts, uint32_t* __restrict__ flags) {
   using F = typename G::F;
   constexpr int XW = 4 * G::CW;
   uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  // the 64-word flag block of the cut sums / cascade that follow on this
+  // stream (instead of a memset launch)
+  if (flags && t < 64) flags[t] = 0;
   if (t >= nchunks) return;
   const uint32_t M = bstart[K];
   uint32_t start = t * L;
@@ -1305,13 +1309,13 @@ __global__ void __launch_bounds__(256, ZK_ACC0_G1_MINBLK) k_msm_acc0_g1(const ui
                                                   const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
                                                   uint32_t* __restrict__ buckets,
                                                   uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                                                  uint32_t* __restrict__ xpts) { msm_acc0_body<G1T>(sval, bstart, K, L, nchunks, bases, tn, tskip, buckets, xkey, xvalid, xpts); }
+                                                  uint32_t* __restrict__ xpts, uint32_t* __restrict__ flags) { msm_acc0_body<G1T>(sval, bstart, K, L, nchunks, bases, tn, tskip, buckets, xkey, xvalid, xpts, flags); }
 __global__ void __launch_bounds__(256, ZK_ACC0_G2_MINBLK) k_msm_acc0_g2(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ bstart,
                                                   uint32_t K, uint32_t L, uint32_t nchunks,
                                                   const uint32_t* __restrict__ bases, uint32_t tn, uint32_t tskip,
                                                   uint32_t* __restrict__ buckets,
                                                   uint32_t* __restrict__ xkey, uint32_t* __restrict__ xvalid,
-                                                  uint32_t* __restrict__ xpts) { msm_acc0_body<G2T>(sval, bstart, K, L, nchunks, bases, tn, tskip, buckets, xkey, xvalid, xpts); }
+                                                  uint32_t* __restrict__ xpts, uint32_t* __restrict__ flags) { msm_acc0_body<G2T>(sval, bstart, K, L, nchunks, bases, tn, tskip, buckets, xkey, xvalid, xpts, flags); }
 template <class G>
 struct Acc0Kernel;
 template <>
@@ -2926,8 +2930,16 @@ static int msm_sort_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const 
     uint32_t *scnt, *scur;
     ZK_TRY(ws.get("msm_ss_cnt", (size_t)P.K * 4, (void**)&scnt));
     ZK_TRY(ws.get("msm_ss_cursor", (size_t)P.K * 4, (void**)&scur));
-    ZK_HIP(hipMemsetAsync(scnt, 0, (size_t)P.K * 4, st));
+    // the counts are left zeroed by the previous counting sort's scan on this
+    // lane, up to lane->ss_clean_words; a new buffer or a larger K is cleared
+    if (scnt != lane->ss_clean || P.K > lane->ss_clean_words) {
+      ZK_HIP(hipMemsetAsync(scnt, 0, (size_t)P.K * 4, st));
+      lane->ss_clean = scnt;
+      lane->ss_clean_words = P.K;
+    }
+    lane->ss_clean = nullptr;  // until every kernel of this sort is queued
     ZK_TRY(small_sort(P.c, P.bal, st, d_scalars, n, P.Wp(), P.B, P.wsel, P.K, scnt, scur, bstart, sval));
+    lane->ss_clean = scnt;
     ZK_HIP(hipEventRecord(lane->consumed, st));
     ZK_HIP(hipStreamWaitEvent(ctx->stream, lane->consumed, 0));
     ZK_HIP(hipGetLastError());
@@ -3173,8 +3185,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     ZK_HIP(hipGetLastError());
   } else {
     uint32_t *flags, *xkey, *xvalid, *xpts, *ykey, *yvalid, *ypts;
-    ZK_TRY(ws.get("msm_flags", 64 * 4, (void**)&flags));
-    ZK_HIP(hipMemsetAsync(flags, 0, 64 * 4, st));
+    ZK_TRY(ws.get("msm_flags", 64 * 4, (void**)&flags));  // zeroed by the accumulation's block 0
     // level 0: fixed-size chunks of the sorted list (sized from the upper bound
     // W*n so no host round-trip is needed; chunks past M exit at once).
     // Threads per CU: measured best at ~1024 for G1 (over-subscribing the
@@ -3193,7 +3204,7 @@ static int msm_acc_phase(zkmi_ctx* ctx, MsmLane* lane, const MsmPlan& P, const z
     {
       ScopedKernelTimer tm(ctx, G::CW == 8 ? "msm_acc0_g1" : "msm_acc0_g2", st);
       Acc0Kernel<G>::fn<<<(nch + 255) / 256, 256, 0, st>>>(sval, bstart, K, L, nch, d_bases, tn, tskip, buckets, xkey,
-                                                            xvalid, xpts);
+                                                            xvalid, xpts, flags);
       ZK_HIP(hipGetLastError());
     }
     ScopedKernelTimer tm(ctx, "msm_accN", st);

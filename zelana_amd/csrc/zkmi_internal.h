@@ -53,6 +53,8 @@ struct MsmLane {
   size_t bs_ctr_words = 0;
   int bs_parity = 0;
   bool bs_dirty = false;  // a sort's kernels were not all queued: clear both blocks next time
+  void* ss_clean = nullptr;   // counting-sort counts known zero in [0, ss_clean_words) (k_ss_scan clears them)
+  size_t ss_clean_words = 0;
   uint32_t* bs_cur = nullptr;
 };
 
