@@ -71,6 +71,25 @@ def test_msm_g1_windows(ctx, c):
     assert np.array_equal(got, O.msm_g1(pts, sc))
 
 
+def test_small_sorts_alternating_bucket_counts(ctx):
+    """The counting sort leaves its counts zeroed for the lane's next small
+    sort (no memset launch) and the accumulation clears the cut-sum flags:
+    alternate the bucket count (window 12 / 13) and the scalar kind on the
+    same lanes, every result against the oracle."""
+    n = 2000
+    pts = O.gen_points_g1(91, n)
+    b = ctx.bases_g1(pts)
+    rng = np.random.default_rng(5)
+    try:
+        for c, kind in [(13, "witness"), (12, "uniform"), (13, "uniform"), (12, "witness"), (13, "edge")]:
+            sc = _rand_scalars(rng, n, kind)
+            ctx.set_window(c)
+            got = ctx.msm(b, sc)
+            assert np.array_equal(got, O.msm_g1(pts, sc)), (c, kind)
+    finally:
+        ctx.set_window(0)
+
+
 def test_msm_g1_degenerate(ctx):
     """repeated bases (doubling path), P and -P (cancellation), infinity bases,
     all-equal scalars (one heavy bucket per window)."""
